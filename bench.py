@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X mCCS allreduce path.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N == 1 (BASELINE.json configs[1]): device-resident chunk reduce, two 128 MiB
+fp32 buffers -> elementwise sum kernel (mccs_hip_reduce).  One step = one
+kernel pass over the 2 x 128 MiB inputs (algorithmic bytes 3 x 128 MiB).
+
+N > 1 (configs[2]; launched by torch.distributed.run, one rank per GPU):
+ring allreduce of a 128 MiB fp32 bucket per rank over xGMI P2P FIFOs
+(mccs_hip allreduce, no RCCL).  One step = one allreduce; value = algbw =
+S / t (reference definition, allreduce_bench/src/main.rs:168).
+
+Prints ONE JSON line on rank 0.  cpu_baseline: the oracle's threaded C
+elementwise sum (oracle/mccs_oracle.c, kind "port") timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident reduce GB/s; ring-allreduce algbw GB/s at 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--size-mib", type=int, default=128)
+    ap.add_argument("--dtype", default="float32", choices=["float32", "float16", "bfloat16"])
+    ap.add_argument("--variant", type=int, default=0, help="reduce main loop: 0 default, 1 REG, 2 LDS")
+    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--policy", type=int, default=-1)
+    ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="interleaved A/B of reduce variants (stderr)")
+    return ap.parse_args()
+
+
+def cpu_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the GPU box's CPU share is 16 per GPU
+
+
+def cpu_baseline(dtype_code: int, nelem: int, budget_s: float) -> dict:
+    """Times the oracle's threaded C elementwise sum on the same workload shape."""
+    import numpy as np
+
+    from oracle import oracle as orc
+
+    npdt = orc.NP_DTYPE[dtype_code]
+    rng = np.random.default_rng(0x6D636373)
+    def gen():
+        f = rng.random(nelem, dtype=np.float32) * 2 - 1
+        if dtype_code == 9:  # bfloat16 stored as raw bits
+            return (f.view(np.uint32) >> 16).astype(np.uint16)
+        return f.astype(npdt)
+
+    a, b = gen(), gen()
+    c = np.empty_like(a)
+    bytes_per = 3 * a.nbytes
+    res = {}
+    for label, nthr, share in (("mt", cpu_threads(), 0.7), ("st", 1, 0.3)):
+        orc.reduce_mt(dtype_code, orc.SUM, [a, b], c, nthr)  # warm (page faults)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            orc.reduce_mt(dtype_code, orc.SUM, [a, b], c, nthr)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s * share and reps >= 2:
+                break
+        res[label] = (bytes_per * reps / el / 1e9, nthr, reps, el)
+    gbps, nthr, reps, el = res["mt"]
+    return {
+        "value": round(gbps, 3),
+        "unit": "GB/s",
+        "cores": nthr,
+        "kind": "port",
+        "sample": f"full workload: {nelem} elems x 2 srcs -> 1 dst, {reps} passes in {el:.2f}s "
+                  f"on {nthr} threads; 1-thread {res['st'][0]:.3f} GB/s ({res['st'][2]} passes)",
+        "single_thread_value": round(res["st"][0], 3),
+    }
+
+
+def load_pmc_traffic(tag: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        v = d.get(tag)
+        return int(v["hbm_bytes_per_launch"]) if v else None
+    except Exception:
+        return None
+
+
+def bench_reduce(args) -> dict:
+    import torch
+
+    import mccs_amd
+    from mccs_amd import DataType
+
+    dt = {"float32": (torch.float32, DataType.Float32), "float16": (torch.float16, DataType.Float16),
+          "bfloat16": (torch.bfloat16, DataType.Bfloat16)}[args.dtype]
+    tdt, code = dt
+    esize = torch.tensor([], dtype=tdt).element_size()
+    nbytes = args.size_mib << 20
+    n = nbytes // esize
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    a = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt)
+    g.manual_seed(2)
+    b = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt)
+    c = torch.empty_like(a)
+    if args.variant or args.unroll or args.policy >= 0 or args.blocks_per_cu:
+        mccs_amd.tune(args.variant, args.unroll, args.policy, args.blocks_per_cu)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+
+    # correctness gate on the exact timed buffers: fp32/fp16/bf16 a+b is one
+    # correctly rounded add, so the torch result is bit-identical
+    step()
+    torch.cuda.synchronize()
+    ref = (a.float() + b.float()).to(tdt) if tdt != torch.float32 else a + b
+    if not torch.equal(c, ref):
+        raise SystemExit("bench_reduce: result mismatch vs a+b")
+
+    if args.sweep:
+        sweep_variants(a, b, c, n, code, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    per_launch_ms = [s.elapsed_time(e) for s, e in ev]
+    total_ms = ev[0][0].elapsed_time(ev[-1][1])
+    alg_bytes = 3 * n * esize
+    avg_launch_s = sum(per_launch_ms) / K / 1e3
+    achieved = alg_bytes / avg_launch_s / 1e9
+    value = alg_bytes * K / (total_ms / 1e3) / 1e9
+    tag = f"reduce_{args.dtype}_{args.size_mib}MiB"
+    traffic = load_pmc_traffic(tag)
+    out = {
+        "metric": METRIC,
+        "submetric": "device_resident_reduce_GBps",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(total_ms / K, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"float32": "f32", "float16": "f16", "bfloat16": "bf16"}[args.dtype],
+        "data": "synthetic uniform[-1,1) seeds 1,2, device-resident",
+        "config": {"workload": f"1-GPU device-resident reduce: two {args.size_mib} MiB {args.dtype} "
+                               f"buffers -> elementwise sum kernel (BASELINE configs[1])",
+                   "elements": n, "bytes_per_step": alg_bytes,
+                   "reduce_tune": mccs_amd.get_tune()},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic, "kernel": "reduce_reg_kernel/reduce_lds_kernel",
+                     "avg_launch_us": round(avg_launch_s * 1e6, 3),
+                     "min_launch_us": round(min(per_launch_ms) * 1e3, 3)},
+        "wall_s": round(wall, 4),
+    }
+    return out
+
+
+def sweep_variants(a, b, c, n, code, stream):
+    """Interleaved rounds of every reduce variant in one process (stderr)."""
+    import torch
+
+    import mccs_amd
+
+    cfgs = []
+    for var in (1, 2):
+        for u in ((2, 4, 8) if var == 1 else (2, 4)):
+            for pol in (0, 1):
+                for bpc in ((2, 4, 8, 16) if var == 1 else (1, 2)):
+                    cfgs.append((var, u, pol, bpc))
+    alg = 3 * c.numel() * c.element_size()
+    times = {cfg: [] for cfg in cfgs}
+    for _ in range(5):
+        for cfg in cfgs:
+            mccs_amd.tune(*cfg)
+            for _ in range(3):
+                mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            for _ in range(10):
+                mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+            e.record(stream)
+            torch.cuda.synchronize()
+            times[cfg].append(s.elapsed_time(e) / 10)
+    rows = sorted(((sorted(v)[len(v) // 2], cfg) for cfg, v in times.items()))
+    for med, cfg in rows:
+        print(f"[sweep] variant={cfg[0]} unroll={cfg[1]} policy={cfg[2]} bpc={cfg[3]} "
+              f"median {med*1e3:.2f} us  {alg/med/1e6:.1f} GB/s", file=sys.stderr)
+    mccs_amd.tune(0, 0, -1, 0)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.gpus > 1:
+        from mccs_amd import ring_bench
+
+        out = ring_bench.run(args)
+        if out is None:  # non-zero rank
+            return
+    else:
+        out = bench_reduce(args)
+        if not args.no_cpu_baseline:
+            from mccs_amd import DataType
+
+            code = {"float32": DataType.Float32, "float16": DataType.Float16,
+                    "bfloat16": DataType.Bfloat16}[args.dtype]
+            esz = 2 if args.dtype != "float32" else 4
+            out["cpu_baseline"] = cpu_baseline(int(code), (args.size_mib << 20) // esz, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

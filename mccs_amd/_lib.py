@@ -1,0 +1,110 @@
+"""ctypes binding of libmccs_hip.so (the C-ABI in include/mccs_hip.h).
+
+The product path has exactly one implementation: the in-tree HIP library.
+If it is missing or fails to load, every call raises -- there is no CPU or
+PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmccs_hip.so")
+
+
+class DataType(enum.IntEnum):
+    """mccsDevDataType_t (reference src/collectives/include/collectives.h:177-192)."""
+
+    Int8 = 0
+    Uint8 = 1
+    Int32 = 2
+    Uint32 = 3
+    Int64 = 4
+    Uint64 = 5
+    Float16 = 6
+    Float32 = 7
+    Float64 = 8
+    Bfloat16 = 9
+
+
+class RedOp(enum.IntEnum):
+    """mccsDevRedOp_t (collectives.h:194-198)."""
+
+    Sum = 0
+    Prod = 1
+    Max = 2
+    Min = 3
+    PreMulSum = 4
+    SumPostDiv = 5
+
+
+ELEM_BYTES = {
+    DataType.Int8: 1, DataType.Uint8: 1, DataType.Int32: 4, DataType.Uint32: 4,
+    DataType.Int64: 8, DataType.Uint64: 8, DataType.Float16: 2, DataType.Float32: 4,
+    DataType.Float64: 8, DataType.Bfloat16: 2,
+}
+
+RESULT_NAMES = {
+    0: "mccsSuccess", 1: "mccsUnhandledCudaError", 2: "mccsSystemError", 3: "mccsInternalError",
+    4: "mccsInvalidArgument", 5: "mccsInvalidUsage", 6: "mccsRemoteError", 7: "mccsInProgress",
+    8: "mccsTimeout",
+}
+
+
+class MccsError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        super().__init__(f"{what}: {RESULT_NAMES.get(code, code)} ({code})")
+
+
+_c_void_p = ctypes.c_void_p
+_c_int = ctypes.c_int
+_c_size_t = ctypes.c_size_t
+_P = ctypes.POINTER
+
+# name -> (restype, argtypes); every symbol declared in include/mccs_hip.h
+SIGNATURES: dict[str, tuple] = {
+    "mccs_hip_version": (ctypes.c_char_p, []),
+    "mccs_hip_reduce": (_c_int, [_c_void_p, _P(_c_void_p), _c_int, _c_size_t, _c_int, _c_int, _c_void_p]),
+    "mccs_hip_reduce_copy": (
+        _c_int,
+        [_P(_c_void_p), _c_int, _P(_c_void_p), _c_int, _c_size_t, _c_int, _c_int, _c_void_p],
+    ),
+    "mccs_hip_reduce_tune": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
+    "mccs_hip_reduce_get_tune": (None, [_P(_c_int), _P(_c_int), _P(_c_int), _P(_c_int)]),
+}
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Loads libmccs_hip.so once; raises if absent (no fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"{p} not found: build it with `python -m mccs_amd.build` (hipcc --offload-arch=gfx950)"
+        )
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        raise MccsError(code, what)
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = ctypes.c_void_p(int(p))
+    return arr

@@ -1,0 +1,116 @@
+"""In-tree build of libmccs_hip.so (gfx950) and the CPU oracle.
+
+``python -m mccs_amd.build`` or ``__graft_entry__.build()``.  Sources are compiled
+one object per file with hipcc (parallel), then linked into
+``mccs_amd/libmccs_hip.so`` so the library travels with the repo snapshot to the
+GPU box.  Objects are cached under ``build/`` keyed on source mtimes.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "mccs_amd")
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+BUILD = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(PKG, "libmccs_hip.so")
+ARCH = os.environ.get("MCCS_OFFLOAD_ARCH", "gfx950")
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+CFLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-Wall",
+    "-Wno-unused-function",
+    "-Wno-unused-variable",
+    f"-I{INCLUDE}",
+    f"-I{CSRC}",
+]
+
+
+def _sources() -> list[str]:
+    out = []
+    for d in (CSRC, os.path.join(CSRC, "host")):
+        if not os.path.isdir(d):
+            continue
+        for f in sorted(os.listdir(d)):
+            if f.endswith((".hip", ".cpp")):
+                out.append(os.path.join(d, f))
+    return out
+
+
+def _headers_mtime() -> float:
+    m = 0.0
+    for d in (CSRC, os.path.join(CSRC, "host"), INCLUDE):
+        if os.path.isdir(d):
+            for f in os.listdir(d):
+                if f.endswith((".h", ".hpp", ".inc")):
+                    m = max(m, os.path.getmtime(os.path.join(d, f)))
+    return m
+
+
+def _obj_for(src: str) -> str:
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
+    return os.path.join(BUILD, rel + ".o")
+
+
+def _compile(src: str, hdr_mtime: float, verbose: bool) -> str:
+    obj = _obj_for(src)
+    if os.path.exists(obj):
+        om = os.path.getmtime(obj)
+        if om >= os.path.getmtime(src) and om >= hdr_mtime:
+            return obj
+    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build_lib(verbose: bool = False, jobs: int | None = None) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    hm = _headers_mtime()
+    jobs = jobs or min(8, max(1, (os.cpu_count() or 2)))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hm, verbose), srcs))
+    newest = max(os.path.getmtime(o) for o in objs)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
+        tmp = LIB + ".tmp"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lpthread"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(verbose: bool = False) -> None:
+    """Builds oracle/libmccs_oracle.so (+ oracle/_ref when the reference tree exists)."""
+    cmd = ["make", "-s", "-C", os.path.join(ROOT, "oracle")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if verbose or r.returncode != 0:
+        print(r.stdout, r.stderr, file=sys.stderr)
+    if r.returncode != 0:
+        raise RuntimeError("oracle build failed")
+
+
+def main() -> None:
+    verbose = "-v" in sys.argv
+    print(build_lib(verbose=verbose))
+    build_oracle(verbose=verbose)
+
+
+if __name__ == "__main__":
+    main()

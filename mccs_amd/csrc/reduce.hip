@@ -1,0 +1,393 @@
+// reduce.hip — device-resident chunk reduce / reduce-copy over a whole MI355X.
+//
+// C-ABI: mccs_hip_reduce / mccs_hip_reduce_copy (include/mccs_hip.h).  This is
+// the standalone form of the reference's per-chunk ReduceOrCopyMulti
+// (src/collectives/src/common_kernel.h:485-685): y = src0 (op) src1 (op) ...
+// stored to every dst, in the element type (reduce_kernel.h functors).  The
+// reference runs that loop inside 1-2 ring blocks; here it is a full-chip,
+// HBM-bound streaming kernel (bytes per element = (nsrcs + ndsts) * sizeof(T),
+// 0.083 flop/B for fp32 2->1: no MFMA).
+//
+// Two main-loop designs, selected at run time (mccs_hip_reduce_tune):
+//   REG  register streaming: each lane keeps U 16-byte packs per source in
+//        flight (global_load_dwordx4), packed VALU op, global_store_dwordx4.
+//   LDS  LDS-DMA staging: each wave streams its sources with
+//        global_load_lds_dwordx4 into an S-stage ring in LDS (S-1 tiles in
+//        flight per wave, counted s_waitcnt vmcnt), reads its own lanes back
+//        with ds_read_b128, applies the op and stores.  Bytes in flight are
+//        bounded by LDS (160 KiB/CU) instead of VGPRs.
+// Grid: persistent, blocks_per_cu * 256 CUs, grid-stride over tiles.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+
+#include "dtypes.h"
+#include "mccs_hip.h"
+#include "reduce_copy.h"
+
+namespace mccs {
+
+constexpr int kMaxSrcs = MCCS_REDUCE_MAX_SRCS;
+constexpr int kMaxDsts = MCCS_REDUCE_MAX_DSTS;
+
+struct ReduceArgs {
+  const void* srcs[kMaxSrcs];
+  void* dsts[kMaxDsts];
+  int nsrcs;
+  int ndsts;
+  int64_t count;
+};
+
+// ---------------------------------------------------------------------------
+// REG: NS/ND > 0 are compile-time source/destination counts; 0 = runtime.
+template <int DT, int OP, int NS, int ND, int U, int LDP, int STP>
+__global__ void __launch_bounds__(256) reduce_reg_kernel(ReduceArgs a) {
+  using T = typename Elem<DT>::T;
+  constexpr int PACK = kPackElems<DT>;
+  constexpr int B = 256;
+  const int nsrcs = NS > 0 ? NS : a.nsrcs;
+  const int ndsts = ND > 0 ? ND : a.ndsts;
+  constexpr int MS = NS > 0 ? NS : kMaxSrcs;
+  constexpr int MD = ND > 0 ? ND : kMaxDsts;
+  const int64_t npack = a.count / PACK;
+  const int64_t tile = (int64_t)B * U;
+  const int tid = threadIdx.x;
+
+  for (int64_t t = blockIdx.x; t * tile < npack; t += gridDim.x) {
+    const int64_t base = t * tile + tid;
+    if ((t + 1) * tile <= npack) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16<LDP>((const u32x4*)a.srcs[0] + base + u * B);
+#pragma unroll
+      for (int s = 1; s < MS; ++s) {
+        if (s < nsrcs) {
+          u32x4 w[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) w[u] = ld16<LDP>((const u32x4*)a.srcs[s] + base + u * B);
+#pragma unroll
+          for (int u = 0; u < U; ++u) v[u] = pack_op<DT, OP>(v[u], w[u]);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < MD; ++d) {
+        if (d < ndsts) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) st16<STP>((u32x4*)a.dsts[d] + base + u * B, v[u]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = base + u * B;
+        if (p < npack) {
+          u32x4 v = ld16<LDP>((const u32x4*)a.srcs[0] + p);
+#pragma unroll
+          for (int s = 1; s < MS; ++s)
+            if (s < nsrcs) v = pack_op<DT, OP>(v, ld16<LDP>((const u32x4*)a.srcs[s] + p));
+#pragma unroll
+          for (int d = 0; d < MD; ++d)
+            if (d < ndsts) st16<STP>((u32x4*)a.dsts[d] + p, v);
+        }
+      }
+    }
+  }
+  // < 16-byte tail: last block, typed scalar
+  if (blockIdx.x == gridDim.x - 1) {
+    for (int64_t e = npack * PACK + tid; e < a.count; e += B) {
+      T v = ((const T*)a.srcs[0])[e];
+      for (int s = 1; s < nsrcs; ++s) v = scalar_op<DT, OP>(v, ((const T*)a.srcs[s])[e]);
+      for (int d = 0; d < ndsts; ++d) ((T*)a.dsts[d])[e] = v;
+    }
+  }
+}
+
+// Unaligned pointers: typed grid-stride loop (reference ReduceCopyMulti path).
+template <int DT, int OP>
+__global__ void __launch_bounds__(256) reduce_scalar_kernel(ReduceArgs a) {
+  using T = typename Elem<DT>::T;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.count; e += stride) {
+    T v = ((const T*)a.srcs[0])[e];
+    for (int s = 1; s < a.nsrcs; ++s) v = scalar_op<DT, OP>(v, ((const T*)a.srcs[s])[e]);
+    for (int d = 0; d < a.ndsts; ++d) ((T*)a.dsts[d])[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LDS: 2 sources -> 1 destination, per-wave LDS-DMA ring of S stages.
+// A wave tile = 64 lanes x U packs per source = U KiB per source.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most nd*G + ns*U vector-memory ops are outstanding (S <= 3)
+template <int G, int U, int S>
+__device__ __forceinline__ void wait_younger(int nd, int ns) {
+  static_assert(S >= 2 && S <= 3, "stages");
+  switch (nd * 4 + ns) {
+    case 0 * 4 + 0: wait_vmcnt<0>(); break;
+    case 0 * 4 + 1: wait_vmcnt<U>(); break;
+    case 0 * 4 + 2: wait_vmcnt<2 * U>(); break;
+    case 1 * 4 + 0: wait_vmcnt<G>(); break;
+    case 1 * 4 + 1: wait_vmcnt<G + U>(); break;
+    case 1 * 4 + 2: wait_vmcnt<G + 2 * U>(); break;
+    case 2 * 4 + 0: wait_vmcnt<2 * G>(); break;
+    case 2 * 4 + 1: wait_vmcnt<2 * G + U>(); break;
+    default: wait_vmcnt<2 * G + 2 * U>(); break;
+  }
+}
+
+// One lane's 16 bytes of a wave-wide LDS-DMA: LDS dst = M0 + lane*16.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_wave_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_wave_base)
+      : "memory");
+}
+
+template <int DT, int OP, int U, int S, int W, int STP>
+__global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
+  constexpr int PACK = kPackElems<DT>;
+  constexpr int G = 2 * U;        // LDS-DMA instructions per wave tile (2 sources)
+  constexpr int STAGE_BYTES = G * 1024;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave_lds =
+      (uint32_t)(uintptr_t)smem + (uint32_t)(wave * S * STAGE_BYTES);
+  const int64_t npack = a.count / PACK;
+  const int64_t wtile = 64 * U;
+  const int64_t ntiles = (npack + wtile - 1) / wtile;
+  const int64_t gw = (int64_t)blockIdx.x * W + wave;  // global wave id
+  const int64_t nw = (int64_t)gridDim.x * W;
+  const u32x4* s0 = (const u32x4*)a.srcs[0];
+  const u32x4* s1 = (const u32x4*)a.srcs[1];
+  u32x4* d0 = (u32x4*)a.dsts[0];
+
+  auto issue = [&](int64_t tile, int stage) {
+    const uint32_t base = wave_lds + (uint32_t)(stage * STAGE_BYTES);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t p = tile * wtile + u * 64 + lane;
+      p = p < npack ? p : npack - 1;  // clamp: partial last tile re-reads a valid pack
+      glds16(s0 + p, base + u * 1024);
+      glds16(s1 + p, base + (U + u) * 1024);
+    }
+  };
+
+  // k-th tile of this wave is gw + k*nw
+  int64_t nmine = gw < ntiles ? (ntiles - gw + nw - 1) / nw : 0;
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nmine) issue(gw + s * nw, s);
+
+  for (int64_t k = 0; k < nmine; ++k) {
+    const int stage = (int)(k % S);
+    const int64_t ahead = k + S - 1;
+    if (ahead < nmine) issue(gw + ahead * nw, (int)(ahead % S));
+    // vmcnt retires in issue order (loads, stores and LDS-DMA together), so
+    // "tile k landed" = at most (younger DMA groups)*G + (younger store
+    // groups)*U operations outstanding.  Younger DMA: tiles k+1..k+S-1 that
+    // exist; younger stores: tiles max(0,k-S+1)..k-1 (stored after tile k's
+    // DMA was issued).  Every tile issues exactly U stores (clamped below).
+    const int nd = (int)((nmine - 1 - k) < (S - 1) ? (nmine - 1 - k) : (S - 1));
+    const int ns = (int)(k < (S - 1) ? k : (S - 1));
+    wait_younger<G, U, S>(nd, ns);
+    const char* st = smem + (size_t)(wave * S + stage) * STAGE_BYTES;
+    const int64_t tbase = (gw + k * nw) * wtile;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      u32x4 x = *(const u32x4*)(st + u * 1024 + lane * 16);
+      u32x4 y = *(const u32x4*)(st + (U + u) * 1024 + lane * 16);
+      int64_t p = tbase + u * 64 + lane;
+      // lanes past the end recompute and rewrite the last pack (same value,
+      // from the same clamped loads) so the store count stays U per tile
+      p = p < npack ? p : npack - 1;
+      st16<STP>(d0 + p, pack_op<DT, OP>(x, y));
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    using T = typename Elem<DT>::T;
+    for (int64_t e = npack * PACK + threadIdx.x; e < a.count; e += W * 64) {
+      T v = scalar_op<DT, OP>(((const T*)a.srcs[0])[e], ((const T*)a.srcs[1])[e]);
+      ((T*)a.dsts[0])[e] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Run-time configuration (process-wide; set before launches).
+struct ReduceTune {
+  int variant = MCCS_REDUCE_VARIANT_REG;
+  int unroll = 4;
+  int policy = 1;  // 1 = non-temporal loads+stores
+  int blocks_per_cu = 8;
+};
+static ReduceTune g_tune;
+static int g_num_cus = 0;
+
+static int num_cus() {
+  if (g_num_cus > 0) return g_num_cus;
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  g_num_cus = n;
+  return n;
+}
+
+template <int DT, int OP, int NS, int ND, int U>
+static hipError_t launch_reg(const ReduceArgs& a, int pol, int grid, hipStream_t st) {
+  if (pol)
+    hipLaunchKernelGGL((reduce_reg_kernel<DT, OP, NS, ND, U, kNonTemporal, kNonTemporal>), dim3(grid),
+                       dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((reduce_reg_kernel<DT, OP, NS, ND, U, kPlain, kPlain>), dim3(grid), dim3(256),
+                       0, st, a);
+  return hipGetLastError();
+}
+
+template <int DT, int OP, int NS, int ND>
+static hipError_t launch_reg_u(const ReduceArgs& a, int u, int pol, int grid, hipStream_t st) {
+  if constexpr (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16) {
+    if (u == 2) return launch_reg<DT, OP, NS, ND, 2>(a, pol, grid, st);
+    if (u == 8) return launch_reg<DT, OP, NS, ND, 8>(a, pol, grid, st);
+  }
+  return launch_reg<DT, OP, NS, ND, 4>(a, pol, grid, st);
+}
+
+template <int DT, int OP, int U, int S>
+static hipError_t launch_lds(const ReduceArgs& a, int pol, int grid, hipStream_t st) {
+  constexpr int W = 4;
+  const size_t lds = (size_t)W * S * 2 * U * 1024;
+  auto kn = reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal>;
+  auto kp = reduce_lds_kernel<DT, OP, U, S, W, kPlain>;
+  static std::atomic<bool> attr_set{false};
+  if (!attr_set.load(std::memory_order_relaxed)) {
+    (void)hipFuncSetAttribute((const void*)kn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set.store(true, std::memory_order_relaxed);
+  }
+  if (pol)
+    hipLaunchKernelGGL(kn, dim3(grid), dim3(W * 64), lds, st, a);
+  else
+    hipLaunchKernelGGL(kp, dim3(grid), dim3(W * 64), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int DT, int OP>
+static hipError_t dispatch(const ReduceArgs& a, hipStream_t st) {
+  constexpr int PACK = kPackElems<DT>;
+  const ReduceTune t = g_tune;
+  const int cus = num_cus();
+  uintptr_t mis = 0;
+  for (int s = 0; s < a.nsrcs; ++s) mis |= (uintptr_t)a.srcs[s];
+  for (int d = 0; d < a.ndsts; ++d) mis |= (uintptr_t)a.dsts[d];
+  if (mis & 15) {
+    int64_t blocks = (a.count + 255) / 256;
+    int grid = (int)(blocks < (int64_t)cus * 8 ? (blocks > 0 ? blocks : 1) : (int64_t)cus * 8);
+    hipLaunchKernelGGL((reduce_scalar_kernel<DT, OP>), dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  const int64_t npack = a.count / PACK;
+  const int64_t tile = 256LL * t.unroll;
+  int64_t tiles = (npack + tile - 1) / tile;
+  if (tiles < 1) tiles = 1;
+  int64_t gmax = (int64_t)cus * (t.blocks_per_cu > 0 ? t.blocks_per_cu : 8);
+  const int grid = (int)(tiles < gmax ? tiles : gmax);
+  if (t.variant == MCCS_REDUCE_VARIANT_LDS && a.nsrcs == 2 && a.ndsts == 1) {
+    if constexpr (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16) {
+      const int S = t.blocks_per_cu >= 2 ? 2 : 3;  // LDS budget: 2 blocks/CU at S=2,U=4
+      if (t.unroll == 2) return S == 2 ? launch_lds<DT, OP, 2, 2>(a, t.policy, grid, st)
+                                       : launch_lds<DT, OP, 2, 3>(a, t.policy, grid, st);
+      return S == 2 ? launch_lds<DT, OP, 4, 2>(a, t.policy, grid, st)
+                    : launch_lds<DT, OP, 4, 3>(a, t.policy, grid, st);
+    }
+  }
+  if (a.nsrcs == 2 && a.ndsts == 1) return launch_reg_u<DT, OP, 2, 1>(a, t.unroll, t.policy, grid, st);
+  if (a.nsrcs == 1 && a.ndsts == 1) return launch_reg_u<DT, OP, 1, 1>(a, t.unroll, t.policy, grid, st);
+  return launch_reg<DT, OP, 0, 0, 4>(a, t.policy, grid, st);
+}
+
+template <int DT>
+static hipError_t dispatch_op(int op, const ReduceArgs& a, hipStream_t st) {
+  switch (op) {
+    case OpSum: return dispatch<DT, OpSum>(a, st);
+    case OpProd: return dispatch<DT, OpProd>(a, st);
+    case OpMax: return dispatch<DT, OpMax>(a, st);
+    case OpMin: return dispatch<DT, OpMin>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+static hipError_t dispatch_all(int dtype, int op, const ReduceArgs& a, hipStream_t st) {
+  switch (dtype) {
+#define X(D) \
+  case D: return dispatch_op<D>(op, a, st);
+    MCCS_FOR_EACH_DTYPE(X)
+#undef X
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace mccs
+
+using namespace mccs;
+
+extern "C" mccsResult_t mccs_hip_reduce_copy(void* const* dsts, int ndsts, const void* const* srcs,
+                                             int nsrcs, size_t count, int dtype, int op,
+                                             hipStream_t stream) {
+  if (nsrcs < 1 || nsrcs > kMaxSrcs || ndsts < 1 || ndsts > kMaxDsts || !srcs || !dsts)
+    return mccsInvalidArgument;
+  if (dtype < 0 || dtype >= mccsNumTypes || op < 0 || op > mccsDevMin) return mccsInvalidArgument;
+  ReduceArgs a{};
+  for (int s = 0; s < nsrcs; ++s) {
+    if (!srcs[s]) return mccsInvalidArgument;
+    a.srcs[s] = srcs[s];
+  }
+  for (int d = 0; d < ndsts; ++d) {
+    if (!dsts[d]) return mccsInvalidArgument;
+    a.dsts[d] = dsts[d];
+  }
+  a.nsrcs = nsrcs;
+  a.ndsts = ndsts;
+  a.count = (int64_t)count;
+  if (count == 0) return mccsSuccess;
+  hipError_t e = dispatch_all(dtype, op, a, stream);
+  return e == hipSuccess ? mccsSuccess : mccsUnhandledCudaError;
+}
+
+extern "C" mccsResult_t mccs_hip_reduce(void* dst, const void* const* srcs, int nsrcs, size_t count,
+                                        int dtype, int op, hipStream_t stream) {
+  void* d[1] = {dst};
+  return mccs_hip_reduce_copy(d, 1, srcs, nsrcs, count, dtype, op, stream);
+}
+
+extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu) {
+  if (variant < 0 || variant > MCCS_REDUCE_VARIANT_LDS) return mccsInvalidArgument;
+  if (unroll != 0 && unroll != 2 && unroll != 4 && unroll != 8) return mccsInvalidArgument;
+  if (variant == MCCS_REDUCE_VARIANT_LDS && unroll == 8) return mccsInvalidArgument;
+  g_tune.variant = variant ? variant : MCCS_REDUCE_VARIANT_REG;
+  g_tune.unroll = unroll ? unroll : 4;
+  g_tune.policy = policy < 0 ? 1 : policy;
+  g_tune.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 8;
+  return mccsSuccess;
+}
+
+extern "C" void mccs_hip_reduce_get_tune(int* variant, int* unroll, int* policy, int* blocks_per_cu) {
+  if (variant) *variant = g_tune.variant;
+  if (unroll) *unroll = g_tune.unroll;
+  if (policy) *policy = g_tune.policy;
+  if (blocks_per_cu) *blocks_per_cu = g_tune.blocks_per_cu;
+}
