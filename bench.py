@@ -41,9 +41,15 @@ def parse():
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--policy", type=int, default=-1)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--stages", type=int, default=0)
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--rotate-mib", type=int, default=1152,
+                    help="rotate over buffer sets totalling >= this many MiB so no step's inputs are "
+                         "resident in the 256 MiB Infinity Cache (0 = reuse one set)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of reduce variants (stderr)")
+    ap.add_argument("--no-hot", action="store_true", help="skip the same-buffer measurement (profiling)")
     return ap.parse_args()
 
 
@@ -125,47 +131,73 @@ def bench_reduce(args) -> dict:
     torch.cuda.set_device(dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    a = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt)
-    g.manual_seed(2)
-    b = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt)
-    c = torch.empty_like(a)
-    if args.variant or args.unroll or args.policy >= 0 or args.blocks_per_cu:
-        mccs_amd.tune(args.variant, args.unroll, args.policy, args.blocks_per_cu)
+    set_bytes = 3 * n * esize
+    nsets = max(1, -(-(args.rotate_mib << 20) // set_bytes)) if args.rotate_mib > 0 else 1
+    sets = []
+    for i in range(nsets):
+        g.manual_seed(2 * i + 1)
+        a_i = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt)
+        g.manual_seed(2 * i + 2)
+        b_i = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt)
+        sets.append((a_i, b_i, torch.empty_like(a_i)))
+    a, b, c = sets[0]
+    if args.variant or args.unroll or args.policy >= 0 or args.blocks_per_cu or args.stages or args.waves:
+        mccs_amd.tune(args.variant, args.unroll, args.policy, args.blocks_per_cu, args.stages, args.waves)
     stream = torch.cuda.current_stream()
+    cur = [0]
 
     def step():
-        mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+        a_, b_, c_ = sets[cur[0] % nsets]
+        cur[0] += 1
+        mccs_amd.reduce(c_, [a_, b_], count=n, dtype=code, stream=stream)
 
     # correctness gate on the exact timed buffers: fp32/fp16/bf16 a+b is one
     # correctly rounded add, so the torch result is bit-identical
-    step()
+    for _ in range(nsets):
+        step()
     torch.cuda.synchronize()
-    ref = (a.float() + b.float()).to(tdt) if tdt != torch.float32 else a + b
-    if not torch.equal(c, ref):
-        raise SystemExit("bench_reduce: result mismatch vs a+b")
+    for a_, b_, c_ in sets:
+        ref = (a_.float() + b_.float()).to(tdt) if tdt != torch.float32 else a_ + b_
+        if not torch.equal(c_, ref):
+            raise SystemExit("bench_reduce: result mismatch vs a+b")
+        del ref
 
     if args.sweep:
-        sweep_variants(a, b, c, n, code, stream)
+        sweep_variants(sets, n, code, stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    t_start.record(stream)
+    for _ in range(K):
         step()
-        e.record(stream)
+    t_end.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    per_launch_ms = [s.elapsed_time(e) for s, e in ev]
-    total_ms = ev[0][0].elapsed_time(ev[-1][1])
+    total_ms = t_start.elapsed_time(t_end)
     alg_bytes = 3 * n * esize
-    avg_launch_s = sum(per_launch_ms) / K / 1e3
+    avg_launch_s = total_ms / K / 1e3  # kernel + same-stream launch boundary
     achieved = alg_bytes / avg_launch_s / 1e9
     value = alg_bytes * K / (total_ms / 1e3) / 1e9
-    tag = f"reduce_{args.dtype}_{args.size_mib}MiB"
+
+    # same-buffer ("hot") rate for reference: inputs may partly stay in the MALL
+    hot_gbps = None
+    if not args.no_hot:
+        for _ in range(3):
+            mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+        hs, he = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        hs.record(stream)
+        for _ in range(20):
+            mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+        he.record(stream)
+        torch.cuda.synchronize()
+        hot_gbps = round(20 * 3 * n * esize / (hs.elapsed_time(he) / 1e3) / 1e9, 2)
+    tune = mccs_amd.get_tune()
+    kernel_name = "reduce_lds_kernel" if tune["variant"] == 2 else "reduce_reg_kernel"
+    tag = f"reduce_{args.dtype}_{args.size_mib}MiB_{kernel_name}"
     traffic = load_pmc_traffic(tag)
     out = {
         "metric": METRIC,
@@ -184,48 +216,63 @@ def bench_reduce(args) -> dict:
         "config": {"workload": f"1-GPU device-resident reduce: two {args.size_mib} MiB {args.dtype} "
                                f"buffers -> elementwise sum kernel (BASELINE configs[1])",
                    "elements": n, "bytes_per_step": alg_bytes,
-                   "reduce_tune": mccs_amd.get_tune()},
+                   "buffer_sets_rotated": nsets,
+                   "same_buffer_GBps": hot_gbps,
+                   "reduce_tune": tune},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic, "kernel": "reduce_reg_kernel/reduce_lds_kernel",
-                     "avg_launch_us": round(avg_launch_s * 1e6, 3),
-                     "min_launch_us": round(min(per_launch_ms) * 1e3, 3)},
+                     "traffic": traffic, "kernel": kernel_name,
+                     "avg_launch_us": round(avg_launch_s * 1e6, 3)},
         "wall_s": round(wall, 4),
     }
     return out
 
 
-def sweep_variants(a, b, c, n, code, stream):
-    """Interleaved rounds of every reduce variant in one process (stderr)."""
+def sweep_variants(sets, n, code, stream):
+    """Interleaved rounds of reduce variants in one process, rotating buffer
+    sets like the timed loop (stderr)."""
     import torch
 
     import mccs_amd
 
     cfgs = []
-    for var in (1, 2):
-        for u in ((2, 4, 8) if var == 1 else (2, 4)):
-            for pol in (0, 1):
-                for bpc in ((2, 4, 8, 16) if var == 1 else (1, 2)):
-                    cfgs.append((var, u, pol, bpc))
-    alg = 3 * c.numel() * c.element_size()
+    for u in (2, 4, 8):  # REG
+        for bpc in (4, 8, 16):
+            cfgs.append((1, u, 1, bpc, 0, 0))
+    for u, s, w in ((1, 2, 4), (1, 3, 4), (1, 4, 4), (2, 2, 4), (2, 3, 4), (2, 4, 4), (4, 2, 4),
+                    (4, 3, 4), (4, 4, 4), (1, 2, 8), (1, 3, 8), (1, 4, 8), (2, 2, 8), (2, 3, 8),
+                    (2, 4, 8), (4, 2, 8)):
+        for bpc in (1, 2):
+            if w * s * 2 * u * bpc <= 160:
+                cfgs.append((2, u, 1, bpc, s, w))
+    cfgs.append((2, 2, 0, 1, 3, 4))
+    cfgs.append((1, 4, 0, 8, 0, 0))
+    c0 = sets[0][2]
+    alg = 3 * c0.numel() * c0.element_size()
     times = {cfg: [] for cfg in cfgs}
+    k = 0
     for _ in range(5):
         for cfg in cfgs:
             mccs_amd.tune(*cfg)
-            for _ in range(3):
-                mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+            for _ in range(2):
+                a_, b_, c_ = sets[k % len(sets)]
+                k += 1
+                mccs_amd.reduce(c_, [a_, b_], count=n, dtype=code, stream=stream)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(stream)
-            for _ in range(10):
-                mccs_amd.reduce(c, [a, b], count=n, dtype=code, stream=stream)
+            for _ in range(12):
+                a_, b_, c_ = sets[k % len(sets)]
+                k += 1
+                mccs_amd.reduce(c_, [a_, b_], count=n, dtype=code, stream=stream)
             e.record(stream)
             torch.cuda.synchronize()
-            times[cfg].append(s.elapsed_time(e) / 10)
-    rows = sorted(((sorted(v)[len(v) // 2], cfg) for cfg, v in times.items()))
-    for med, cfg in rows:
-        print(f"[sweep] variant={cfg[0]} unroll={cfg[1]} policy={cfg[2]} bpc={cfg[3]} "
-              f"median {med*1e3:.2f} us  {alg/med/1e6:.1f} GB/s", file=sys.stderr)
-    mccs_amd.tune(0, 0, -1, 0)
+            times[cfg].append(s.elapsed_time(e) / 12)
+    rows = sorted(((sorted(v)[len(v) // 2], min(v), cfg) for cfg, v in times.items()))
+    for med, mn, cfg in rows:
+        print(f"[sweep] variant={cfg[0]} unroll={cfg[1]} policy={cfg[2]} bpc={cfg[3]} stages={cfg[4]} "
+              f"waves={cfg[5]} median {med*1e3:.2f} us  {alg/med/1e6:.1f} GB/s  (best {alg/mn/1e6:.1f})",
+              file=sys.stderr)
+    mccs_amd.tune()
 
 
 def main():

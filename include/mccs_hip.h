@@ -54,10 +54,15 @@ mccsResult_t mccs_hip_reduce(void *dst, const void *const *srcs, int nsrcs, size
                              int op, hipStream_t stream);
 mccsResult_t mccs_hip_reduce_copy(void *const *dsts, int ndsts, const void *const *srcs, int nsrcs,
                                   size_t count, int dtype, int op, hipStream_t stream);
-/* Select main loop, unroll (2/4/8, 0 = default), cache policy (0 plain,
- * 1 non-temporal, -1 default) and persistent blocks per CU (0 = default). */
-mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu);
-void mccs_hip_reduce_get_tune(int *variant, int *unroll, int *policy, int *blocks_per_cu);
+/* Select the main loop (0 = default), unroll = KiB per source per wave tile
+ * for LDS / 16-byte packs per lane for REG (1/2/4/8, 0 = default), cache
+ * policy (0 plain, 1 non-temporal, -1 default), persistent blocks per CU,
+ * LDS ring stages (2..4) and waves per block (4/8); 0 = default for each.
+ * Process-wide; for benchmarking and tests. */
+mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu, int stages,
+                                  int waves);
+void mccs_hip_reduce_get_tune(int *variant, int *unroll, int *policy, int *blocks_per_cu, int *stages,
+                              int *waves);
 
 /* Library identification. */
 const char *mccs_hip_version(void);

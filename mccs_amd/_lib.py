@@ -72,8 +72,8 @@ SIGNATURES: dict[str, tuple] = {
         _c_int,
         [_P(_c_void_p), _c_int, _P(_c_void_p), _c_int, _c_size_t, _c_int, _c_int, _c_void_p],
     ),
-    "mccs_hip_reduce_tune": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
-    "mccs_hip_reduce_get_tune": (None, [_P(_c_int), _P(_c_int), _P(_c_int), _P(_c_int)]),
+    "mccs_hip_reduce_tune": (_c_int, [_c_int] * 6),
+    "mccs_hip_reduce_get_tune": (None, [_P(_c_int)] * 6),
 }
 
 _lib = None

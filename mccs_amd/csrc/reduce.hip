@@ -125,21 +125,22 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// wait until at most nd*G + ns*U vector-memory ops are outstanding (S <= 3)
+// wait until at most nd*G + ns*U vector-memory ops are outstanding
+// (nd, ns < S <= 4; vmcnt immediates must be compile-time constants)
 template <int G, int U, int S>
 __device__ __forceinline__ void wait_younger(int nd, int ns) {
-  static_assert(S >= 2 && S <= 3, "stages");
+  static_assert(S >= 2 && S <= 4, "stages");
+  static_assert((S - 1) * (G + U) < 64, "vmcnt range");
+#define MCCS_WY(ND, NS) \
+  case (ND) * 4 + (NS): wait_vmcnt<(ND) * G + (NS) * U>(); break;
   switch (nd * 4 + ns) {
-    case 0 * 4 + 0: wait_vmcnt<0>(); break;
-    case 0 * 4 + 1: wait_vmcnt<U>(); break;
-    case 0 * 4 + 2: wait_vmcnt<2 * U>(); break;
-    case 1 * 4 + 0: wait_vmcnt<G>(); break;
-    case 1 * 4 + 1: wait_vmcnt<G + U>(); break;
-    case 1 * 4 + 2: wait_vmcnt<G + 2 * U>(); break;
-    case 2 * 4 + 0: wait_vmcnt<2 * G>(); break;
-    case 2 * 4 + 1: wait_vmcnt<2 * G + U>(); break;
-    default: wait_vmcnt<2 * G + 2 * U>(); break;
+    MCCS_WY(0, 0) MCCS_WY(0, 1) MCCS_WY(0, 2) MCCS_WY(0, 3)
+    MCCS_WY(1, 0) MCCS_WY(1, 1) MCCS_WY(1, 2) MCCS_WY(1, 3)
+    MCCS_WY(2, 0) MCCS_WY(2, 1) MCCS_WY(2, 2) MCCS_WY(2, 3)
+    MCCS_WY(3, 0) MCCS_WY(3, 1) MCCS_WY(3, 2)
+    default: wait_vmcnt<0>(); break;
   }
+#undef MCCS_WY
 }
 
 // One lane's 16 bytes of a wave-wide LDS-DMA: LDS dst = M0 + lane*16.
@@ -227,12 +228,20 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Run-time configuration (process-wide; set before launches).
+// Run-time configuration (process-wide; set before launches).  Defaults are
+// the fastest measured on MI355X with inputs streamed from HBM (bench.py
+// --sweep with buffer rotation, profiles/r01_*): REG main loop, 4 packs per
+// source per lane, 16 blocks of 256 per CU, non-temporal loads and stores
+// (6.39 TB/s).  The LDS-DMA loop (U=2, 3 stages, 4 waves, 1 block/CU) is
+// faster only when the inputs are Infinity-Cache resident (7.27 vs 6.59
+// TB/s same-buffer) and slower from HBM (5.92 TB/s); see DESIGN.md.
 struct ReduceTune {
   int variant = MCCS_REDUCE_VARIANT_REG;
   int unroll = 4;
   int policy = 1;  // 1 = non-temporal loads+stores
-  int blocks_per_cu = 8;
+  int blocks_per_cu = 16;
+  int stages = 3;
+  int waves = 4;
 };
 static ReduceTune g_tune;
 static int g_num_cus = 0;
@@ -260,16 +269,19 @@ static hipError_t launch_reg(const ReduceArgs& a, int pol, int grid, hipStream_t
 
 template <int DT, int OP, int NS, int ND>
 static hipError_t launch_reg_u(const ReduceArgs& a, int u, int pol, int grid, hipStream_t st) {
-  if constexpr (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16) {
+  if constexpr (OP == OpSum && (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16)) {
     if (u == 2) return launch_reg<DT, OP, NS, ND, 2>(a, pol, grid, st);
     if (u == 8) return launch_reg<DT, OP, NS, ND, 8>(a, pol, grid, st);
   }
   return launch_reg<DT, OP, NS, ND, 4>(a, pol, grid, st);
 }
 
-template <int DT, int OP, int U, int S>
-static hipError_t launch_lds(const ReduceArgs& a, int pol, int grid, hipStream_t st) {
-  constexpr int W = 4;
+template <int U, int S, int W>
+constexpr bool lds_fits() { return W * S * 2 * U <= 160; }  // KiB of LDS per block
+
+template <int DT, int OP, int U, int S, int W>
+static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t st) {
+  static_assert(lds_fits<U, S, W>(), "LDS budget");
   const size_t lds = (size_t)W * S * 2 * U * 1024;
   auto kn = reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal>;
   auto kp = reduce_lds_kernel<DT, OP, U, S, W, kPlain>;
@@ -279,11 +291,36 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int grid, hipStream_t
     (void)hipFuncSetAttribute((const void*)kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set.store(true, std::memory_order_relaxed);
   }
+  constexpr int PACK = kPackElems<DT>;
+  const int64_t npack = a.count / PACK;
+  const int64_t wtiles = (npack + 64 * U - 1) / (64 * U);
+  int64_t blocks = (wtiles + W - 1) / W;
+  const int64_t gmax = (int64_t)num_cus() * bpc;
+  const int grid = (int)(blocks < gmax ? (blocks > 0 ? blocks : 1) : gmax);
   if (pol)
     hipLaunchKernelGGL(kn, dim3(grid), dim3(W * 64), lds, st, a);
   else
     hipLaunchKernelGGL(kp, dim3(grid), dim3(W * 64), lds, st, a);
   return hipGetLastError();
+}
+
+// (U, S, W) run-time -> template.  The default (2, 3, 4) exists for every
+// dtype/op; the tuning grid only for Sum over fp32/fp16/bf16.
+template <int DT, int OP>
+static hipError_t launch_lds_cfg(const ReduceArgs& a, const ReduceTune& t, bool* ok, hipStream_t st) {
+  *ok = true;
+#define MCCS_LDS(U, S, W) \
+  if (t.unroll == U && t.stages == S && t.waves == W) return launch_lds<DT, OP, U, S, W>(a, t.policy, t.blocks_per_cu, st);
+  MCCS_LDS(2, 3, 4)
+  if constexpr (OP == OpSum && (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16)) {
+    MCCS_LDS(1, 2, 4) MCCS_LDS(1, 3, 4) MCCS_LDS(1, 4, 4) MCCS_LDS(2, 2, 4) MCCS_LDS(2, 4, 4)
+    MCCS_LDS(4, 2, 4) MCCS_LDS(4, 3, 4) MCCS_LDS(4, 4, 4)
+    MCCS_LDS(1, 2, 8) MCCS_LDS(1, 3, 8) MCCS_LDS(1, 4, 8) MCCS_LDS(2, 2, 8) MCCS_LDS(2, 3, 8)
+    MCCS_LDS(2, 4, 8) MCCS_LDS(4, 2, 8)
+  }
+#undef MCCS_LDS
+  *ok = false;
+  return hipSuccess;
 }
 
 template <int DT, int OP>
@@ -300,23 +337,22 @@ static hipError_t dispatch(const ReduceArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((reduce_scalar_kernel<DT, OP>), dim3(grid), dim3(256), 0, st, a);
     return hipGetLastError();
   }
+  if (t.variant == MCCS_REDUCE_VARIANT_LDS && a.nsrcs == 2 && a.ndsts == 1) {
+    bool ok = false;
+    hipError_t e = launch_lds_cfg<DT, OP>(a, t, &ok, st);
+    if (ok) return e;
+    // untuned (U,S,W) for this dtype/op: fall through to the REG loop
+  }
+  const int unroll = t.variant == MCCS_REDUCE_VARIANT_REG ? t.unroll : 4;
+  const int bpc = t.variant == MCCS_REDUCE_VARIANT_REG ? t.blocks_per_cu : 16;
   const int64_t npack = a.count / PACK;
-  const int64_t tile = 256LL * t.unroll;
+  const int64_t tile = 256LL * unroll;
   int64_t tiles = (npack + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
-  int64_t gmax = (int64_t)cus * (t.blocks_per_cu > 0 ? t.blocks_per_cu : 8);
+  const int64_t gmax = (int64_t)cus * (bpc > 0 ? bpc : 8);
   const int grid = (int)(tiles < gmax ? tiles : gmax);
-  if (t.variant == MCCS_REDUCE_VARIANT_LDS && a.nsrcs == 2 && a.ndsts == 1) {
-    if constexpr (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16) {
-      const int S = t.blocks_per_cu >= 2 ? 2 : 3;  // LDS budget: 2 blocks/CU at S=2,U=4
-      if (t.unroll == 2) return S == 2 ? launch_lds<DT, OP, 2, 2>(a, t.policy, grid, st)
-                                       : launch_lds<DT, OP, 2, 3>(a, t.policy, grid, st);
-      return S == 2 ? launch_lds<DT, OP, 4, 2>(a, t.policy, grid, st)
-                    : launch_lds<DT, OP, 4, 3>(a, t.policy, grid, st);
-    }
-  }
-  if (a.nsrcs == 2 && a.ndsts == 1) return launch_reg_u<DT, OP, 2, 1>(a, t.unroll, t.policy, grid, st);
-  if (a.nsrcs == 1 && a.ndsts == 1) return launch_reg_u<DT, OP, 1, 1>(a, t.unroll, t.policy, grid, st);
+  if (a.nsrcs == 2 && a.ndsts == 1) return launch_reg_u<DT, OP, 2, 1>(a, unroll, t.policy, grid, st);
+  if (a.nsrcs == 1 && a.ndsts == 1) return launch_reg_u<DT, OP, 1, 1>(a, unroll, t.policy, grid, st);
   return launch_reg<DT, OP, 0, 0, 4>(a, t.policy, grid, st);
 }
 
@@ -374,20 +410,32 @@ extern "C" mccsResult_t mccs_hip_reduce(void* dst, const void* const* srcs, int 
   return mccs_hip_reduce_copy(d, 1, srcs, nsrcs, count, dtype, op, stream);
 }
 
-extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu) {
+extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu,
+                                             int stages, int waves) {
   if (variant < 0 || variant > MCCS_REDUCE_VARIANT_LDS) return mccsInvalidArgument;
-  if (unroll != 0 && unroll != 2 && unroll != 4 && unroll != 8) return mccsInvalidArgument;
-  if (variant == MCCS_REDUCE_VARIANT_LDS && unroll == 8) return mccsInvalidArgument;
-  g_tune.variant = variant ? variant : MCCS_REDUCE_VARIANT_REG;
-  g_tune.unroll = unroll ? unroll : 4;
-  g_tune.policy = policy < 0 ? 1 : policy;
-  g_tune.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 8;
+  if (unroll < 0 || unroll > 8 || (unroll & (unroll - 1))) return mccsInvalidArgument;
+  if (stages < 0 || stages == 1 || stages > 4 || waves < 0 || (waves != 0 && waves != 4 && waves != 8))
+    return mccsInvalidArgument;
+  ReduceTune d;
+  ReduceTune t;
+  t.variant = variant ? variant : d.variant;
+  const bool reg = t.variant == MCCS_REDUCE_VARIANT_REG;
+  t.unroll = unroll ? unroll : (reg ? 4 : 2);
+  t.policy = policy < 0 ? d.policy : (policy ? 1 : 0);
+  t.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : (reg ? 16 : 1);
+  t.stages = stages ? stages : d.stages;
+  t.waves = waves ? waves : d.waves;
+  if (!reg && t.waves * t.stages * 2 * t.unroll > 160) return mccsInvalidArgument;
+  g_tune = t;
   return mccsSuccess;
 }
 
-extern "C" void mccs_hip_reduce_get_tune(int* variant, int* unroll, int* policy, int* blocks_per_cu) {
+extern "C" void mccs_hip_reduce_get_tune(int* variant, int* unroll, int* policy, int* blocks_per_cu,
+                                         int* stages, int* waves) {
   if (variant) *variant = g_tune.variant;
   if (unroll) *unroll = g_tune.unroll;
   if (policy) *policy = g_tune.policy;
   if (blocks_per_cu) *blocks_per_cu = g_tune.blocks_per_cu;
+  if (stages) *stages = g_tune.stages;
+  if (waves) *waves = g_tune.waves;
 }

@@ -67,13 +67,17 @@ def reduce(dst, srcs, count: int | None = None, dtype=None, op=RedOp.Sum, stream
     reduce_copy([dst], srcs, count=count, dtype=dtype, op=op, stream=stream)
 
 
-def tune(variant: int = 0, unroll: int = 0, policy: int = -1, blocks_per_cu: int = 0) -> None:
-    _lib.check(_lib.load().mccs_hip_reduce_tune(variant, unroll, policy, blocks_per_cu), "mccs_hip_reduce_tune")
+def tune(variant: int = 0, unroll: int = 0, policy: int = -1, blocks_per_cu: int = 0,
+         stages: int = 0, waves: int = 0) -> None:
+    """Process-wide main-loop selection (0 / -1 = default for each field)."""
+    _lib.check(_lib.load().mccs_hip_reduce_tune(variant, unroll, policy, blocks_per_cu, stages, waves),
+               "mccs_hip_reduce_tune")
 
 
 def get_tune() -> dict:
     import ctypes
 
-    v, u, p, b = (ctypes.c_int() for _ in range(4))
-    _lib.load().mccs_hip_reduce_get_tune(ctypes.byref(v), ctypes.byref(u), ctypes.byref(p), ctypes.byref(b))
-    return {"variant": v.value, "unroll": u.value, "policy": p.value, "blocks_per_cu": b.value}
+    vals = [ctypes.c_int() for _ in range(6)]
+    _lib.load().mccs_hip_reduce_get_tune(*(ctypes.byref(v) for v in vals))
+    keys = ("variant", "unroll", "policy", "blocks_per_cu", "stages", "waves")
+    return {k: v.value for k, v in zip(keys, vals)}

@@ -134,20 +134,21 @@ def test_invalid_arguments_fail_loudly():
         mccs_amd.reduce(a, [a, a], op=4)  # PreMulSum is not compiled (reference gen_rules.sh:15)
 
 
-@pytest.mark.parametrize("variant,unroll,policy,bpc", [
-    (1, 2, 0, 4), (1, 4, 1, 8), (1, 8, 1, 2), (2, 2, 0, 1), (2, 4, 1, 1), (2, 4, 1, 2), (2, 2, 1, 2)])
+@pytest.mark.parametrize("variant,unroll,policy,bpc,stages,waves", [
+    (1, 2, 0, 4, 0, 0), (1, 4, 1, 8, 0, 0), (1, 8, 1, 2, 0, 0), (2, 2, 0, 1, 3, 4), (2, 4, 1, 1, 3, 4),
+    (2, 4, 1, 2, 2, 4), (2, 1, 1, 1, 4, 8), (2, 2, 1, 2, 4, 4), (2, 4, 1, 1, 4, 4), (2, 2, 1, 1, 2, 8)])
 @pytest.mark.parametrize("code", [6, 7, 9])
-def test_reduce_variants(orc, variant, unroll, policy, bpc, code):
+def test_reduce_variants(orc, variant, unroll, policy, bpc, stages, waves, code):
     import mccs_amd
 
     rng = np.random.default_rng(variant * 100 + unroll)
     n = (3 << 20) + 123  # many tiles per wave + partial last tile + scalar tail
     srcs = [rand(code, n, rng) for _ in range(2)]
-    mccs_amd.tune(variant, unroll, policy, bpc)
+    mccs_amd.tune(variant, unroll, policy, bpc, stages, waves)
     try:
         (got,) = run_reduce(srcs, 1, code, 0)
     finally:
-        mccs_amd.tune(0, 0, -1, 0)
+        mccs_amd.tune()
     (ref,) = orc.reduce_copy(code, 0, srcs)
     assert np.array_equal(got.view(np.uint8), ref.view(np.uint8))
 
@@ -165,7 +166,7 @@ def test_reduce_full_benchmark_size(orc):
     b = torch.rand(n, device="cuda", generator=g) * 2 - 1
     c = torch.empty_like(a)
     for variant in (1, 2):
-        mccs_amd.tune(variant, 0, -1, 0)
+        mccs_amd.tune(variant)
         c.zero_()
         mccs_amd.reduce(c, [a, b])
         torch.cuda.synchronize()
@@ -173,4 +174,4 @@ def test_reduce_full_benchmark_size(orc):
         ref = np.empty_like(ha)
         orc.reduce_mt(7, 0, [ha, hb], ref, 8)
         assert np.array_equal(c.cpu().numpy().view(np.uint32), ref.view(np.uint32)), variant
-    mccs_amd.tune(0, 0, -1, 0)
+    mccs_amd.tune()
