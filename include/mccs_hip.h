@@ -64,6 +64,95 @@ mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int block
 void mccs_hip_reduce_get_tune(int *variant, int *unroll, int *policy, int *blocks_per_cu, int *stages,
                               int *waves);
 
+/* ======================================================================
+ * Ring collectives: device kernels (reference src/collectives) and the
+ * host runtime that plans and launches them (reference src/mccs/src/proxy,
+ * comm, transport; src/libmccs).
+ * ====================================================================== */
+
+/* Host stub of the reference-named kernel mccsKernel_<Func>_RING_SIMPLE_<Op>_<T>
+ * (collectives.h:43-49) for hipLaunchKernel: the value plan.rs:142-166 stores
+ * in KernelPlan.kernel_fn.  func: mccsFuncAllReduce | mccsFuncAllGather. */
+const void *mccs_hip_coll_kernel(int func, int dtype, int op);
+/* plan.rs:638-669 launch_plan: hipLaunchKernel(fn, grid, block, {comm,
+ * channelMask, workHead}, 0, stream).  grid = #channels * lanes. */
+mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, struct mccsDevComm *comm, uint64_t channelMask,
+                                  struct mccsDevWork *workHead, unsigned grid, unsigned block,
+                                  hipStream_t stream);
+
+typedef struct mccsComm *mccsComm_t;
+
+#define MCCS_LOCALITY_SENDER 0   /* FIFO data in the sender's HBM; receiver reads over xGMI */
+#define MCCS_LOCALITY_RECEIVER 1 /* FIFO data in the receiver's HBM; sender writes over xGMI */
+#define MCCS_FIFO_UNCACHED 0     /* hipDeviceMallocUncached arena: no L2 maintenance needed */
+#define MCCS_FIFO_DEVICE 1       /* hipMalloc arena + system-scope release/acquire */
+
+/* Communicator profile: comm_default_config (mccs.toml:18-20, config.rs:15-97)
+ * plus the MI355X execution knobs.  Zero fields take defaults. */
+typedef struct {
+  int channel_count;    /* rings; 0 = auto: 2 x edge-disjoint Hamiltonian cycles of the node */
+  int buffer_size;      /* FIFO bytes per connection (buffer_sizes[0]); 0 = 4 MiB */
+  int lanes;            /* workgroups per channel; 0 = auto */
+  int block_threads;    /* threads per workgroup (64..1024); 0 = 512 */
+  int locality;         /* MCCS_LOCALITY_*; default SENDER (reference shm default) */
+  int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED */
+  int timeout_ms;       /* FIFO spin watchdog; 0 = 30000, < 0 = never */
+  int work_fifo_depth;  /* mccsDevWork slots (power of two); 0 = 4096 */
+  int bridge_streams;   /* 1 (default): user stream -> comm stream events (libmccs semantics); -1: launch on user stream */
+  const int *rings;     /* channel_count x nranks send orders (comm_patterns_override); NULL = auto */
+} mccsCommConfig;
+
+void mccsCommConfigDefault(mccsCommConfig *cfg);
+
+/* One process drives `nranks` ranks (the reference service model: one mccs
+ * process owns every GPU of the host).  devices[r] is rank r's GPU; devices
+ * may repeat (several ranks on one GPU: their collectives must be issued
+ * inside one mccsGroupStart/End so they run as one launch). */
+mccsResult_t mccsCommInitAll(mccsComm_t *comms, int nranks, const int *devices, const mccsCommConfig *cfg);
+
+/* One rank per process: SetupRank allocates this rank's FIFO arena and writes
+ * a connect handle (IPC memory handle + layout, mccsConnectHandleSize()
+ * bytes); the caller all-gathers the handles out of band (the reference's
+ * bootstrap/exchange engines) and passes all nranks of them, concatenated in
+ * rank order, to Connect. */
+size_t mccsConnectHandleSize(void);
+mccsResult_t mccsCommSetupRank(mccsComm_t *comm, int rank, int nranks, int device, const mccsCommConfig *cfg,
+                               void *handle_out);
+mccsResult_t mccsCommConnect(mccsComm_t comm, const void *all_handles);
+
+/* libmccs::all_reduce (src/libmccs/src/collectives.rs:75-138): count in
+ * elements of dtype, stream-ordered on `stream`, returns after launch. */
+mccsResult_t mccsAllReduce(const void *sendbuff, void *recvbuff, size_t count, int dtype, int op, mccsComm_t comm,
+                           hipStream_t stream);
+/* libmccs::all_gather: sendbytes per rank; recvbuff holds nranks*sendbytes. */
+mccsResult_t mccsAllGather(const void *sendbuff, void *recvbuff, size_t sendbytes, mccsComm_t comm,
+                           hipStream_t stream);
+/* Group calls (ProxyCommand::GroupCall): collectives issued between Start and
+ * End are planned together and launched at End (one launch per device). */
+mccsResult_t mccsGroupStart(void);
+mccsResult_t mccsGroupEnd(void);
+
+/* Waits for the comm's stream and reports a device-side failure (watchdog
+ * timeout / abort) as mccsTimeout / mccsRemoteError. */
+mccsResult_t mccsCommSync(mccsComm_t comm);
+/* Raises the comm's abortFlag: in-flight kernels exit at their next poll. */
+mccsResult_t mccsCommAbort(mccsComm_t comm);
+mccsResult_t mccsCommDestroy(mccsComm_t comm);
+/* rank, nranks, device, channels, lanes, block threads, fifo memory kind. */
+mccsResult_t mccsCommInfo(mccsComm_t comm, int *info7);
+/* ring send order of channel ch (nranks ints). */
+mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int *order);
+/* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
+mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
+const char *mccsGetErrorString(mccsResult_t r);
+
+/* Host-only helpers (no GPU needed). */
+/* Default ring orders for an n-rank node (edge-disjoint Hamiltonian cycles,
+ * both directions); writes up to max_channels x nranks ints, returns count. */
+int mccs_default_rings(int nranks, int nch_req, int *out, int max_channels);
+/* get_task_schema (plan.rs:602-635): channels and threads for total_bytes. */
+void mccs_task_schema(size_t total_bytes, int nch_cfg, int *nch, int *nthreads);
+
 /* Library identification. */
 const char *mccs_hip_version(void);
 

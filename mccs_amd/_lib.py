@@ -64,6 +64,15 @@ _c_int = ctypes.c_int
 _c_size_t = ctypes.c_size_t
 _P = ctypes.POINTER
 
+class _CommConfig(ctypes.Structure):
+    """mccsCommConfig (include/mccs_hip.h)."""
+
+    _fields_ = [("channel_count", _c_int), ("buffer_size", _c_int), ("lanes", _c_int),
+                ("block_threads", _c_int), ("locality", _c_int), ("fifo_memory", _c_int),
+                ("timeout_ms", _c_int), ("work_fifo_depth", _c_int), ("bridge_streams", _c_int),
+                ("rings", _P(_c_int))]
+
+
 # name -> (restype, argtypes); every symbol declared in include/mccs_hip.h
 SIGNATURES: dict[str, tuple] = {
     "mccs_hip_version": (ctypes.c_char_p, []),
@@ -74,6 +83,29 @@ SIGNATURES: dict[str, tuple] = {
     ),
     "mccs_hip_reduce_tune": (_c_int, [_c_int] * 6),
     "mccs_hip_reduce_get_tune": (None, [_P(_c_int)] * 6),
+    # ring kernels + communicator runtime
+    "mccs_hip_coll_kernel": (_c_void_p, [_c_int, _c_int, _c_int]),
+    "mccs_hip_launch_coll": (
+        _c_int, [_c_int, _c_int, _c_int, _c_void_p, ctypes.c_uint64, _c_void_p, ctypes.c_uint, ctypes.c_uint,
+                 _c_void_p]),
+    "mccsCommConfigDefault": (None, [_P(_CommConfig)]),
+    "mccsCommInitAll": (_c_int, [_P(_c_void_p), _c_int, _P(_c_int), _P(_CommConfig)]),
+    "mccsConnectHandleSize": (_c_size_t, []),
+    "mccsCommSetupRank": (_c_int, [_P(_c_void_p), _c_int, _c_int, _c_int, _P(_CommConfig), _c_void_p]),
+    "mccsCommConnect": (_c_int, [_c_void_p, _c_void_p]),
+    "mccsAllReduce": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_int, _c_int, _c_void_p, _c_void_p]),
+    "mccsAllGather": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p, _c_void_p]),
+    "mccsGroupStart": (_c_int, []),
+    "mccsGroupEnd": (_c_int, []),
+    "mccsCommSync": (_c_int, [_c_void_p]),
+    "mccsCommAbort": (_c_int, [_c_void_p]),
+    "mccsCommDestroy": (_c_int, [_c_void_p]),
+    "mccsCommInfo": (_c_int, [_c_void_p, _P(_c_int)]),
+    "mccsCommRing": (_c_int, [_c_void_p, _c_int, _P(_c_int)]),
+    "mccsCommDevComm": (_c_int, [_c_void_p, _P(_c_void_p)]),
+    "mccsGetErrorString": (ctypes.c_char_p, [_c_int]),
+    "mccs_default_rings": (_c_int, [_c_int, _c_int, _P(_c_int), _c_int]),
+    "mccs_task_schema": (None, [_c_size_t, _c_int, _P(_c_int), _P(_c_int)]),
 }
 
 _lib = None

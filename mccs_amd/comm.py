@@ -1,0 +1,233 @@
+"""Communicators and collectives: the Python face of libmccs.
+
+Mirrors the reference application API (src/libmccs/src/lib.rs:19-27):
+
+  reference (Rust libmccs)                      here
+  ------------------------------------------    ---------------------------------------------
+  init_communicator_rank(id, rank, n, dev, ip)  init_communicator_rank(rank, n, dev, exchange)
+  all_reduce(comm, send, recv, size, dtype,     all_reduce(comm, send, recv, size, dtype,
+             op, stream) -> Result<(), Error>              op, stream)  (raises MccsError)
+  all_gather(comm, send, recv, size, stream)    all_gather(comm, send, recv, size, stream)
+  AllReduceDataType {Float16, Int32}            AllReduceDataType (+ Float32: the one API delta,
+                                                SURVEY §8(b); + the other kernel dtypes)
+  AllReduceOpType {Sum, Prod, ...}              AllReduceOpType
+
+`size` is an element count (src/ipc/mccs/src/command.rs:71-80).  Everything
+below is a thin ctypes layer over include/mccs_hip.h; the work happens in
+libmccs_hip.so (HIP kernels + C++ planner).  There is no fallback path.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import enum
+from dataclasses import dataclass
+
+from . import _lib
+from ._lib import DataType, RedOp, _CommConfig
+
+_P = ctypes.POINTER
+_vp, _ci, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+
+
+class AllReduceDataType(enum.IntEnum):
+    """ipc::mccs::command::AllReduceDataType (command.rs:28-31) + Float32 and the
+    remaining kernel dtypes; values are mccsDevDataType_t codes."""
+
+    Float16 = DataType.Float16
+    Int32 = DataType.Int32
+    Float32 = DataType.Float32
+    Int8 = DataType.Int8
+    Uint8 = DataType.Uint8
+    Uint32 = DataType.Uint32
+    Int64 = DataType.Int64
+    Uint64 = DataType.Uint64
+    Float64 = DataType.Float64
+    Bfloat16 = DataType.Bfloat16
+
+
+class AllReduceOpType(enum.IntEnum):
+    """command.rs:33-42 (PreMulSum/SumPostDiv are declared there but no kernel
+    exists for them in the reference either: gen_rules.sh:15)."""
+
+    Sum = 0
+    Prod = 1
+    Max = 2
+    Min = 3
+    PreMulSum = 4
+    SumPostDiv = 5
+
+
+LOCALITY_SENDER, LOCALITY_RECEIVER = 0, 1
+FIFO_UNCACHED, FIFO_DEVICE = 0, 1
+
+
+@dataclass
+class CommConfig:
+    """comm_default_config (mccs.toml:18-20) + MI355X knobs; 0 = library default."""
+
+    channel_count: int = 0
+    buffer_size: int = 0
+    lanes: int = 0
+    block_threads: int = 0
+    locality: int = LOCALITY_SENDER
+    fifo_memory: int = FIFO_UNCACHED
+    timeout_ms: int = 0
+    work_fifo_depth: int = 0
+    bridge_streams: int = 1
+    rings: list | None = None  # comm_patterns_override: channel_count x nranks send orders
+
+    def to_c(self, nranks: int):
+        c = _CommConfig()
+        for f, _ in _CommConfig._fields_:
+            if f != "rings":
+                setattr(c, f, int(getattr(self, f)))
+        keep = None
+        if self.rings is not None:
+            flat = [int(x) for ring in self.rings for x in ring]
+            if len(flat) != len(self.rings) * nranks:
+                raise ValueError("each ring must list every rank once")
+            keep = (_ci * len(flat))(*flat)
+            c.rings = ctypes.cast(keep, _P(_ci))
+            c.channel_count = len(self.rings)
+        return c, keep
+
+
+def _sig():
+    return _lib.load()
+
+
+def _ptr(x) -> int:
+    return x.data_ptr() if hasattr(x, "data_ptr") else int(x)
+
+
+def _stream(s) -> int:
+    if s is None:
+        import torch
+
+        return torch.cuda.current_stream().cuda_stream
+    return s.cuda_stream if hasattr(s, "cuda_stream") else int(s)
+
+
+class Communicator:
+    """One rank of a communicator (reference: MccsCommunicatorHandle)."""
+
+    def __init__(self, handle: int):
+        self._h = ctypes.c_void_p(handle)
+        info = (_ci * 7)()
+        _lib.check(_sig().mccsCommInfo(self._h, info), "mccsCommInfo")
+        (self.rank, self.nranks, self.device, self.nchannels, self.lanes, self.block_threads,
+         self.fifo_memory) = list(info)
+
+    @property
+    def handle(self) -> int:
+        return self._h.value
+
+    def rings(self) -> list[list[int]]:
+        out = []
+        for ch in range(self.nchannels):
+            arr = (_ci * self.nranks)()
+            _lib.check(_sig().mccsCommRing(self._h, ch, arr), "mccsCommRing")
+            out.append(list(arr))
+        return out
+
+    def dev_comm(self) -> int:
+        p = ctypes.c_void_p()
+        _lib.check(_sig().mccsCommDevComm(self._h, ctypes.byref(p)), "mccsCommDevComm")
+        return p.value
+
+    def all_reduce(self, send_buf, recv_buf, size: int, data_type=AllReduceDataType.Float32,
+                   op_type=AllReduceOpType.Sum, stream=None) -> None:
+        all_reduce(self, send_buf, recv_buf, size, data_type, op_type, stream)
+
+    def all_gather(self, send_buf, recv_buf, size: int, stream=None) -> None:
+        all_gather(self, send_buf, recv_buf, size, stream)
+
+    def sync(self) -> None:
+        """Waits for the comm's launches; raises on a device-side timeout/abort."""
+        _lib.check(_sig().mccsCommSync(self._h), "mccsCommSync")
+
+    def abort(self) -> None:
+        _lib.check(_sig().mccsCommAbort(self._h), "mccsCommAbort")
+
+    def destroy(self) -> None:
+        if self._h.value:
+            _lib.check(_sig().mccsCommDestroy(self._h), "mccsCommDestroy")
+            self._h = ctypes.c_void_p(0)
+
+
+def init_all(devices: list[int], config: CommConfig | None = None) -> list[Communicator]:
+    """One process drives len(devices) ranks (the reference's one-service-per-host
+    model).  Devices may repeat: ranks sharing a GPU must issue collectives
+    inside `group()` so they run as one launch."""
+    lib = _sig()
+    n = len(devices)
+    cfg, keep = (config or CommConfig()).to_c(n)
+    hs = (_vp * n)()
+    devs = (_ci * n)(*devices)
+    _lib.check(lib.mccsCommInitAll(hs, n, devs, ctypes.byref(cfg)), "mccsCommInitAll")
+    del keep
+    return [Communicator(hs[i]) for i in range(n)]
+
+
+def init_communicator_rank(rank: int, nranks: int, device: int, exchange, config: CommConfig | None = None):
+    """One rank per process.  `exchange(bytes) -> list[bytes]` all-gathers the
+    per-rank connect handles (e.g. over torch.distributed/gloo); it replaces
+    the reference's bootstrap ring + exchange engine."""
+    lib = _sig()
+    cfg, keep = (config or CommConfig()).to_c(nranks)
+    hsize = lib.mccsConnectHandleSize()
+    mine = (ctypes.c_char * hsize)()
+    h = ctypes.c_void_p()
+    _lib.check(lib.mccsCommSetupRank(ctypes.byref(h), rank, nranks, device, ctypes.byref(cfg), mine),
+               "mccsCommSetupRank")
+    del keep
+    allh = exchange(bytes(mine))
+    if len(allh) != nranks or any(len(x) != hsize for x in allh):
+        raise RuntimeError("connect-handle exchange returned malformed data")
+    buf = ctypes.create_string_buffer(b"".join(allh), hsize * nranks)
+    _lib.check(lib.mccsCommConnect(h, buf), "mccsCommConnect")
+    return Communicator(h.value)
+
+
+def all_reduce(comm: Communicator, send_buf, recv_buf, size: int, data_type=AllReduceDataType.Float32,
+               op_type=AllReduceOpType.Sum, stream=None) -> None:
+    """libmccs::all_reduce (collectives.rs:75-138): stream-ordered, returns after launch."""
+    rc = _sig().mccsAllReduce(_ptr(send_buf), _ptr(recv_buf), int(size), int(data_type), int(op_type),
+                              comm._h, _stream(stream))
+    _lib.check(rc, "mccsAllReduce")
+
+
+def all_gather(comm: Communicator, send_buf, recv_buf, size: int, stream=None) -> None:
+    """libmccs::all_gather: `size` bytes per rank; recv holds nranks*size bytes."""
+    rc = _sig().mccsAllGather(_ptr(send_buf), _ptr(recv_buf), int(size), comm._h, _stream(stream))
+    _lib.check(rc, "mccsAllGather")
+
+
+@contextlib.contextmanager
+def group():
+    """ProxyCommand::GroupCall: collectives inside are launched together at exit."""
+    lib = _sig()
+    _lib.check(lib.mccsGroupStart(), "mccsGroupStart")
+    try:
+        yield
+    finally:
+        _lib.check(lib.mccsGroupEnd(), "mccsGroupEnd")
+
+
+def default_rings(nranks: int, channels: int = 0) -> list[list[int]]:
+    """Default ring orders (host-only; no GPU needed)."""
+    out = (_ci * (32 * nranks))()
+    k = _sig().mccs_default_rings(nranks, channels, out, 32)
+    return [list(out[c * nranks:(c + 1) * nranks]) for c in range(k)]
+
+
+def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
+    a, b = _ci(), _ci()
+    _sig().mccs_task_schema(total_bytes, channels, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+__all__ = ["AllReduceDataType", "AllReduceOpType", "CommConfig", "Communicator", "init_all",
+           "init_communicator_rank", "all_reduce", "all_gather", "group", "default_rings", "task_schema",
+           "RedOp", "DataType"]

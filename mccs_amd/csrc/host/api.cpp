@@ -1,0 +1,384 @@
+// api.cpp — extern "C" communicator / collective API of libmccs_hip.so.
+//
+// The reference splits this across libmccs (app shim, src/libmccs/src/*.rs),
+// the daemon relay and the proxy engine; here the app calls the planner
+// directly (no daemon process on the hot path: the reference's WR/WC shared
+// memory queues only relay the same arguments, collectives.rs:88-131).
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "comm.h"
+#include "dtypes.h"
+
+namespace mccs {
+void task_schema(size_t total_bytes, int nch_cfg, int* nch_out, int* nthreads_out);
+
+struct GroupState {
+  int depth = 0;
+  mccsResult_t error = mccsSuccess;  // first failure inside the group
+  std::vector<Comm*> comms;
+  std::vector<hipStream_t> streams;
+};
+
+// Drops every plan queued in the current group (error path).
+static void group_discard() {
+  for (Comm* c : g_group.comms) {
+    for (auto& s : c->sched) s = ChannelSchedule{};
+    c->plan_pending = false;
+  }
+  g_group.comms.clear();
+  g_group.streams.clear();
+}
+static thread_local GroupState g_group;
+
+static void fill_defaults(mccsCommConfig* c) {
+  if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
+  if (c->block_threads <= 0) c->block_threads = 512;
+  if (c->work_fifo_depth <= 0) c->work_fifo_depth = 4096;
+  if (c->bridge_streams == 0) c->bridge_streams = 1;
+}
+
+static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
+  if (c.buffer_size < 64 * MCCS_BUFFER_SLOTS || c.buffer_size % (256 * MCCS_BUFFER_SLOTS) != 0)
+    return mccsInvalidArgument;
+  // multiples of 32 keep the reference's nWarps*32 blocks (e.g. 544) valid
+  if (c.block_threads < 64 || c.block_threads > 1024 || c.block_threads % 32) return mccsInvalidArgument;
+  if (c.lanes < 0 || c.lanes > MCCS_MAX_LANES) return mccsInvalidArgument;
+  if (c.channel_count < 0 || c.channel_count > MCCS_MAX_NCHANNELS) return mccsInvalidArgument;
+  if (c.work_fifo_depth & (c.work_fifo_depth - 1)) return mccsInvalidArgument;
+  if (c.locality != MCCS_LOCALITY_SENDER && c.locality != MCCS_LOCALITY_RECEIVER) return mccsInvalidArgument;
+  if (c.fifo_memory != MCCS_FIFO_UNCACHED && c.fifo_memory != MCCS_FIFO_DEVICE) return mccsInvalidArgument;
+  if (nranks < 1 || nranks > 64) return mccsInvalidArgument;
+  return mccsSuccess;
+}
+
+static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommConfig* user_cfg, Comm** out) {
+  mccsCommConfig cfg;
+  mccsCommConfigDefault(&cfg);
+  if (user_cfg) cfg = *user_cfg;
+  fill_defaults(&cfg);
+  MCCS_CHECK(validate_cfg(cfg, nranks));
+  if (rank < 0 || rank >= nranks) return mccsInvalidArgument;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return mccsInvalidArgument;
+  Comm* c = new Comm();
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = device;
+  c->cfg = cfg;
+  if (cfg.rings) {
+    const int nch = cfg.channel_count > 0 ? cfg.channel_count : 1;
+    for (int ch = 0; ch < nch; ++ch) {
+      std::vector<int> r(cfg.rings + (size_t)ch * nranks, cfg.rings + (size_t)(ch + 1) * nranks);
+      std::vector<int> s = r;
+      std::sort(s.begin(), s.end());
+      for (int i = 0; i < nranks; ++i)
+        if (s[i] != i) {
+          delete c;
+          return mccsInvalidArgument;  // not a permutation (engine.rs:274-279 asserts)
+        }
+      c->rings.push_back(r);
+    }
+  } else {
+    default_rings(nranks, cfg.channel_count, &c->rings);
+  }
+  c->cfg.rings = nullptr;  // not owned
+  c->nch = (int)c->rings.size();
+  c->block_threads = cfg.block_threads;
+  c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, 16 / c->nch)));
+  *out = c;
+  return mccsSuccess;
+}
+
+static mccsResult_t enable_peer(int a, int b) {
+  if (a == b) return mccsSuccess;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) return mccsSystemError;
+  DeviceGuard g(a);
+  hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+    MCCS_LOG("hipDeviceEnablePeerAccess(%d -> %d): %s", a, b, hipGetErrorString(e));
+    return mccsUnhandledCudaError;
+  }
+  (void)hipGetLastError();
+  return mccsSuccess;
+}
+
+static mccsResult_t launch_single(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count,
+                                  hipStream_t stream) {
+  auto reject = [](mccsResult_t e) {
+    if (g_group.depth > 0 && g_group.error == mccsSuccess) g_group.error = e;
+    return e;
+  };
+  if (!c || !c->connected) return reject(mccsInvalidUsage);
+  if (c->failed) return reject(mccsRemoteError);
+  if (count == 0) return mccsSuccess;
+  if (!send || !recv) return reject(mccsInvalidArgument);
+  if (func == mccsFuncAllReduce && (dtype < 0 || dtype >= mccsNumTypes || op < 0 || op > mccsDevMin))
+    return reject(mccsInvalidArgument);
+  if (std::find(g_group.comms.begin(), g_group.comms.end(), c) == g_group.comms.end()) {
+    g_group.comms.push_back(c);
+    g_group.streams.push_back(stream);
+  }
+  mccsResult_t er = plan_enqueue(c, func, dtype, op, send, recv, count);
+  if (er != mccsSuccess) {
+    if (g_group.depth == 0) group_discard();
+    else if (g_group.error == mccsSuccess) g_group.error = er;
+    return er;
+  }
+  if (g_group.depth == 0) {
+    mccsResult_t r = plan_launch_group(g_group.comms, g_group.streams);
+    g_group.comms.clear();
+    g_group.streams.clear();
+    return r;
+  }
+  return mccsSuccess;
+}
+
+}  // namespace mccs
+
+using namespace mccs;
+
+extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->buffer_size = 1 << 22;
+  cfg->block_threads = 512;
+  cfg->locality = MCCS_LOCALITY_SENDER;
+  cfg->fifo_memory = MCCS_FIFO_UNCACHED;
+  cfg->work_fifo_depth = 4096;
+  cfg->bridge_streams = 1;
+}
+
+extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {
+  if (!comms || !devices || nranks < 1) return mccsInvalidArgument;
+  std::vector<Comm*> cs(nranks, nullptr);
+  mccsResult_t r = mccsSuccess;
+  for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = make_comm(i, nranks, devices[i], cfg, &cs[i]);
+  for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_alloc_local(cs[i]);
+  for (int i = 0; i < nranks && r == mccsSuccess; ++i)
+    for (int j = 0; j < nranks && r == mccsSuccess; ++j) r = enable_peer(devices[i], devices[j]);
+  if (r == mccsSuccess) {
+    bool all_uc = true;
+    for (int i = 0; i < nranks; ++i) all_uc = all_uc && cs[i]->own_arena_uncached;
+    for (int i = 0; i < nranks; ++i) {
+      for (int j = 0; j < nranks; ++j) cs[i]->peer_arena[j] = cs[j]->own_arena;
+      cs[i]->all_uncached = all_uc;
+    }
+    for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_build_device(cs[i]);
+  }
+  if (r != mccsSuccess) {
+    for (auto c : cs)
+      if (c) {
+        comm_free(c);
+        delete c;
+      }
+    return r;
+  }
+  for (int i = 0; i < nranks; ++i) comms[i] = (mccsComm_t)cs[i];
+  return mccsSuccess;
+}
+
+extern "C" size_t mccsConnectHandleSize(void) { return sizeof(ConnectHandle); }
+
+extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks, int device, const mccsCommConfig* cfg,
+                                          void* handle_out) {
+  if (!out || !handle_out) return mccsInvalidArgument;
+  Comm* c = nullptr;
+  MCCS_CHECK(make_comm(rank, nranks, device, cfg, &c));
+  mccsResult_t r = comm_alloc_local(c);
+  ConnectHandle h;
+  std::memset(&h, 0, sizeof(h));
+  if (r == mccsSuccess) {
+    DeviceGuard g(device);
+    hipError_t e = hipIpcGetMemHandle(&h.ipc, c->own_arena);
+    if (e != hipSuccess && c->own_arena_uncached) {
+      // IPC export of the uncached arena refused: fall back to a plain device arena
+      MCCS_LOG("hipIpcGetMemHandle(uncached arena): %s; retrying with hipMalloc", hipGetErrorString(e));
+      (void)hipGetLastError();
+      (void)hipFree(c->own_arena);
+      c->own_arena = nullptr;
+      c->own_arena_uncached = false;
+      e = hipMalloc((void**)&c->own_arena, c->layout.total());
+      if (e == hipSuccess) e = hipMemset(c->own_arena, 0, c->layout.total());
+      if (e == hipSuccess) e = hipIpcGetMemHandle(&h.ipc, c->own_arena);
+      c->peer_arena[rank] = c->own_arena;
+    }
+    if (e != hipSuccess) {
+      MCCS_LOG("hipIpcGetMemHandle: %s", hipGetErrorString(e));
+      r = mccsUnhandledCudaError;
+    }
+  }
+  if (r != mccsSuccess) {
+    comm_free(c);
+    delete c;
+    return r;
+  }
+  h.magic = kHandleMagic;
+  h.rank = rank;
+  h.nranks = nranks;
+  h.device = device;
+  h.pid = (int32_t)getpid();
+  h.fifo_memory = c->own_arena_uncached ? MCCS_FIFO_UNCACHED : MCCS_FIFO_DEVICE;
+  h.nch = c->nch;
+  h.arena_bytes = c->layout.total();
+  h.buffer_size = c->layout.buffer_size;
+  gethostname(h.host, sizeof(h.host) - 1);
+  std::memcpy(handle_out, &h, sizeof(h));
+  *out = (mccsComm_t)c;
+  return mccsSuccess;
+}
+
+extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles) {
+  Comm* c = (Comm*)comm;
+  if (!c || !all_handles || c->connected) return mccsInvalidUsage;
+  const ConnectHandle* hs = (const ConnectHandle*)all_handles;
+  bool all_uc = true;
+  for (int r = 0; r < c->nranks; ++r) {
+    const ConnectHandle& h = hs[r];
+    if (h.magic != kHandleMagic || h.rank != r || h.nranks != c->nranks || h.nch != c->nch ||
+        h.arena_bytes != c->layout.total() || h.buffer_size != c->layout.buffer_size)
+      return mccsInvalidArgument;  // ranks disagree on the communicator profile
+    all_uc = all_uc && h.fifo_memory == MCCS_FIFO_UNCACHED;
+  }
+  DeviceGuard g(c->device);
+  for (int r = 0; r < c->nranks; ++r) {
+    if (r == c->rank) continue;
+    const ConnectHandle& h = hs[r];
+    if (h.pid == (int32_t)getpid()) return mccsInvalidUsage;  // same process: use mccsCommInitAll
+    (void)enable_peer(c->device, h.device);                    // best effort; IPC maps regardless
+    void* p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, h.ipc, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      MCCS_LOG("hipIpcOpenMemHandle(rank %d): %s", r, hipGetErrorString(e));
+      return mccsUnhandledCudaError;
+    }
+    c->peer_arena[r] = (char*)p;
+    c->peer_opened_ipc[r] = true;
+  }
+  c->all_uncached = all_uc;
+  return comm_build_device(c);
+}
+
+extern "C" mccsResult_t mccsAllReduce(const void* sendbuff, void* recvbuff, size_t count, int dtype, int op,
+                                      mccsComm_t comm, hipStream_t stream) {
+  return launch_single((Comm*)comm, mccsFuncAllReduce, dtype, op, sendbuff, recvbuff, count, stream);
+}
+
+extern "C" mccsResult_t mccsAllGather(const void* sendbuff, void* recvbuff, size_t sendbytes, mccsComm_t comm,
+                                      hipStream_t stream) {
+  return launch_single((Comm*)comm, mccsFuncAllGather, mccsInt8, mccsDevSum, sendbuff, recvbuff, sendbytes, stream);
+}
+
+extern "C" mccsResult_t mccsGroupStart(void) {
+  ++g_group.depth;
+  return mccsSuccess;
+}
+
+extern "C" mccsResult_t mccsGroupEnd(void) {
+  if (g_group.depth <= 0) return mccsInvalidUsage;
+  if (--g_group.depth > 0) return mccsSuccess;
+  if (g_group.error != mccsSuccess) {  // a collective of the group was rejected: launch none
+    const mccsResult_t e = g_group.error;
+    g_group.error = mccsSuccess;
+    group_discard();
+    return e;
+  }
+  mccsResult_t r = plan_launch_group(g_group.comms, g_group.streams);
+  g_group.comms.clear();
+  g_group.streams.clear();
+  return r;
+}
+
+extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
+  Comm* c = (Comm*)comm;
+  if (!c) return mccsInvalidArgument;
+  DeviceGuard g(c->device);
+  MCCS_HIP(hipEventSynchronize(c->event));
+  MCCS_HIP(hipStreamSynchronize(c->stream));
+  unsigned err = 0;
+  MCCS_HIP(ring_take_device_error(&err));
+  uint32_t abort_val = 0;
+  MCCS_HIP(hipMemcpy(&abort_val, c->d_abort, sizeof(abort_val), hipMemcpyDeviceToHost));
+  if (err || abort_val) c->failed = true;
+  if (err & MCCS_ERR_TIMEOUT) return mccsTimeout;
+  if (err || abort_val) return mccsRemoteError;
+  return mccsSuccess;
+}
+
+extern "C" mccsResult_t mccsCommAbort(mccsComm_t comm) {
+  Comm* c = (Comm*)comm;
+  if (!c) return mccsInvalidArgument;
+  DeviceGuard g(c->device);
+  const uint32_t one = 1;
+  MCCS_HIP(hipMemcpy(c->d_abort, &one, sizeof(one), hipMemcpyHostToDevice));
+  c->failed = true;
+  return mccsSuccess;
+}
+
+extern "C" mccsResult_t mccsCommDestroy(mccsComm_t comm) {
+  Comm* c = (Comm*)comm;
+  if (!c) return mccsInvalidArgument;
+  comm_free(c);
+  delete c;
+  return mccsSuccess;
+}
+
+extern "C" mccsResult_t mccsCommInfo(mccsComm_t comm, int* info) {
+  Comm* c = (Comm*)comm;
+  if (!c || !info) return mccsInvalidArgument;
+  info[0] = c->rank;
+  info[1] = c->nranks;
+  info[2] = c->device;
+  info[3] = c->nch;
+  info[4] = c->lanes;
+  info[5] = c->block_threads;
+  info[6] = c->all_uncached ? MCCS_FIFO_UNCACHED : MCCS_FIFO_DEVICE;
+  return mccsSuccess;
+}
+
+extern "C" mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int* order) {
+  Comm* c = (Comm*)comm;
+  if (!c || !order || ch < 0 || ch >= c->nch) return mccsInvalidArgument;
+  for (int i = 0; i < c->nranks; ++i) order[i] = c->rings[ch][i];
+  return mccsSuccess;
+}
+
+extern "C" mccsResult_t mccsCommDevComm(mccsComm_t comm, void** dev_comm) {
+  Comm* c = (Comm*)comm;
+  if (!c || !dev_comm) return mccsInvalidArgument;
+  *dev_comm = c->d_comm;
+  return mccsSuccess;
+}
+
+extern "C" const char* mccsGetErrorString(mccsResult_t r) {
+  switch (r) {
+    case mccsSuccess: return "no error";
+    case mccsUnhandledCudaError: return "unhandled HIP error";
+    case mccsSystemError: return "system error";
+    case mccsInternalError: return "internal error";
+    case mccsInvalidArgument: return "invalid argument";
+    case mccsInvalidUsage: return "invalid usage";
+    case mccsRemoteError: return "remote process exited or the kernel aborted";
+    case mccsInProgress: return "in progress";
+    case mccsTimeout: return "FIFO watchdog timeout";
+    default: return "unknown result";
+  }
+}
+
+// Pure host helpers, usable without a GPU (tests, tools).
+extern "C" int mccs_default_rings(int nranks, int nch_req, int* out, int max_channels) {
+  std::vector<std::vector<int>> rings;
+  default_rings(nranks, nch_req, &rings);
+  int n = std::min((int)rings.size(), max_channels);
+  for (int c = 0; c < n; ++c)
+    for (int i = 0; i < nranks; ++i) out[c * nranks + i] = rings[c][i];
+  return n;
+}
+
+extern "C" void mccs_task_schema(size_t total_bytes, int nch_cfg, int* nch, int* nthreads) {
+  task_schema(total_bytes, nch_cfg, nch, nthreads);
+}

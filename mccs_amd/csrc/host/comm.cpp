@@ -1,0 +1,214 @@
+// comm.cpp — communicator resources, ring patterns and xGMI FIFO connectors.
+//
+// Reference counterparts:
+//   ring user_ranks / index ..... src/mccs/src/proxy/engine.rs:269-320
+//   CommDevResources::new ....... src/mccs/src/comm/device.rs:81-183
+//   conn_info_to_dev ............ src/mccs/src/comm/device.rs:35-52
+//   SHM connector setup ......... src/mccs/src/transport/shm/transporter.rs:49-183
+// The SHM connector's host-pinned FIFO (cudaHostRegister'd, PCIe) is replaced
+// by one per-rank HBM arena holding, per channel, the FIFO data of one
+// connection and the head/tail flag lines; peers reach it over xGMI through
+// peer access (same process) or IPC (one rank per process).
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+
+#include "comm.h"
+
+namespace mccs {
+
+// ---------------------------------------------------------------------------
+// Ring patterns.  Default topology for one fully connected MI355X node:
+// edge-disjoint Hamiltonian cycles of K_n (greedy DFS, deterministic so every
+// rank derives the same rings), each used in both directions, so the rings
+// spread over n-2 or n-1 of the n-1 xGMI links of every GPU instead of one.
+static bool ham_dfs(int n, std::vector<std::vector<char>>& used, std::vector<int>& path,
+                    std::vector<char>& seen) {
+  if ((int)path.size() == n) return !used[path.back()][path[0]];
+  const int u = path.back();
+  for (int k = 1; k < n; ++k) {
+    const int v = (u + k) % n;  // rotate neighbour order: spreads early cycles
+    if (seen[v] || used[u][v]) continue;
+    seen[v] = 1;
+    path.push_back(v);
+    if (ham_dfs(n, used, path, seen)) return true;
+    path.pop_back();
+    seen[v] = 0;
+  }
+  return false;
+}
+
+void default_rings(int n, int nch_req, std::vector<std::vector<int>>* rings) {
+  rings->clear();
+  std::vector<std::vector<int>> base;
+  if (n <= 2) {
+    std::vector<int> r(n);
+    for (int i = 0; i < n; ++i) r[i] = i;
+    base.push_back(r);
+  } else if (n == 4) {
+    // K4 has no two edge-disjoint Hamiltonian cycles; its three cycles cover
+    // every edge exactly twice, so all six directed rings load links evenly.
+    base = {{0, 1, 2, 3}, {0, 3, 2, 1}, {0, 2, 1, 3}, {0, 3, 1, 2}, {0, 1, 3, 2}, {0, 2, 3, 1}};
+  } else {
+    std::vector<std::vector<char>> used(n, std::vector<char>(n, 0));
+    for (int k = 0; k < n; ++k) {
+      std::vector<int> path{0};
+      std::vector<char> seen(n, 0);
+      seen[0] = 1;
+      if (!ham_dfs(n, used, path, seen)) break;
+      for (int i = 0; i < n; ++i) {
+        const int a = path[i], b = path[(i + 1) % n];
+        used[a][b] = used[b][a] = 1;
+      }
+      base.push_back(path);
+      std::vector<int> rev{0};
+      for (int i = n - 1; i >= 1; --i) rev.push_back(path[i]);
+      base.push_back(rev);
+    }
+    if (base.empty()) {
+      std::vector<int> r(n);
+      for (int i = 0; i < n; ++i) r[i] = i;
+      base.push_back(r);
+    }
+  }
+  int nch = nch_req > 0 ? nch_req : (n <= 2 ? 2 : (int)base.size());
+  nch = std::min(nch, (int)MCCS_MAX_NCHANNELS);
+  for (int c = 0; c < nch; ++c) rings->push_back(base[c % base.size()]);
+}
+
+// ---------------------------------------------------------------------------
+mccsResult_t comm_set_kernel_cfg(Comm* c) {
+  mccsRingKernelCfg k{};
+  k.fence_mode = c->all_uncached ? MCCS_FENCE_UNCACHED : MCCS_FENCE_SYSTEM;
+  const int tmo = c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms;
+  k.timeout_ticks = tmo < 0 ? 0 : (uint64_t)tmo * 100000ull;  // s_memrealtime: 100 MHz
+  DeviceGuard g(c->device);
+  MCCS_HIP(ring_set_device_cfg(k));
+  return mccsSuccess;
+}
+
+mccsResult_t comm_alloc_local(Comm* c) {
+  DeviceGuard g(c->device);
+  c->layout.nch = c->nch;
+  c->layout.buffer_size = (size_t)c->cfg.buffer_size;
+  const size_t bytes = c->layout.total();
+  c->own_arena = nullptr;
+  c->own_arena_uncached = false;
+  if (c->cfg.fifo_memory == MCCS_FIFO_UNCACHED) {
+    hipError_t e = hipExtMallocWithFlags((void**)&c->own_arena, bytes, hipDeviceMallocUncached);
+    if (e == hipSuccess) {
+      c->own_arena_uncached = true;
+    } else {
+      (void)hipGetLastError();
+      MCCS_LOG("uncached FIFO arena unavailable (%s); using hipMalloc + system fences", hipGetErrorString(e));
+      c->own_arena = nullptr;
+    }
+  }
+  if (!c->own_arena) MCCS_HIP(hipMalloc((void**)&c->own_arena, bytes));
+  MCCS_HIP(hipMemset(c->own_arena, 0, bytes));
+  c->peer_arena.assign(c->nranks, nullptr);
+  c->peer_opened_ipc.assign(c->nranks, false);
+  c->peer_arena[c->rank] = c->own_arena;
+
+  MCCS_HIP(hipMalloc((void**)&c->d_abort, 64));
+  MCCS_HIP(hipMemset(c->d_abort, 0, 64));  // the reference leaves it uninitialised (device.rs:157)
+  MCCS_HIP(hipMalloc((void**)&c->d_comm, sizeof(mccsDevCommAndChannels)));
+  c->d_peers.assign(c->nch, nullptr);
+  c->d_user_ranks.assign(c->nch, nullptr);
+  for (int ch = 0; ch < c->nch; ++ch) {
+    MCCS_HIP(hipMalloc((void**)&c->d_peers[ch], sizeof(mccsDevChannelPeer) * c->nranks));
+    MCCS_HIP(hipMalloc((void**)&c->d_user_ranks[ch], sizeof(int) * c->nranks));
+  }
+  c->work_depth = (uint32_t)c->cfg.work_fifo_depth;
+  MCCS_HIP(hipHostMalloc((void**)&c->h_work, sizeof(mccsDevWork) * c->work_depth, hipHostMallocMapped));
+  MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_work, c->h_work, 0));
+  std::memset(c->h_work, 0, sizeof(mccsDevWork) * c->work_depth);
+  MCCS_HIP(hipHostMalloc((void**)&c->h_done, sizeof(uint32_t) * MCCS_MAX_NCHANNELS, hipHostMallocMapped));
+  MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_done, c->h_done, 0));
+  std::memset(c->h_done, 0, sizeof(uint32_t) * MCCS_MAX_NCHANNELS);
+  c->chan_next.assign(c->nch, 0);
+  c->work_next = 0;
+  c->work_acked_min = 0;
+  MCCS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  MCCS_HIP(hipEventCreateWithFlags(&c->event, hipEventDisableTiming));
+  MCCS_HIP(hipEventCreateWithFlags(&c->user_event, hipEventDisableTiming));
+  c->sched.assign(c->nch, ChannelSchedule{});
+  return mccsSuccess;
+}
+
+// Builds mccsDevCommAndChannels once every peer arena is reachable
+// (CommDevResources::new, device.rs:81-183; ring fields engine.rs:274-286).
+mccsResult_t comm_build_device(Comm* c) {
+  DeviceGuard g(c->device);
+  const int n = c->nranks;
+  mccsDevCommAndChannels hc;
+  std::memset(&hc, 0, sizeof(hc));
+  hc.comm.rank = c->rank;
+  hc.comm.nRanks = n;
+  hc.comm.buffSizes[MCCS_PROTO_SIMPLE] = c->cfg.buffer_size;
+  hc.comm.abortFlag = c->d_abort;
+  for (int ch = 0; ch < c->nch; ++ch) {
+    const std::vector<int>& ring = c->rings[ch];
+    const int ix_rank = (int)(std::find(ring.begin(), ring.end(), c->rank) - ring.begin());
+    const int ix_zero = (int)(std::find(ring.begin(), ring.end(), 0) - ring.begin());
+    std::vector<int> user_ranks(n);
+    for (int i = 0; i < n; ++i) user_ranks[i] = ring[(i + ix_rank) % n];
+    const int prev = user_ranks[n - 1], next = n > 1 ? user_ranks[1] : user_ranks[0];
+    std::vector<mccsDevChannelPeer> peers(n);
+    std::memset(peers.data(), 0, sizeof(mccsDevChannelPeer) * n);
+    if (n > 1) {
+      const bool sender_local = c->cfg.locality == MCCS_LOCALITY_SENDER;
+      char* me = c->peer_arena[c->rank];
+      char* nx = c->peer_arena[next];
+      char* pv = c->peer_arena[prev];
+      if (!me || !nx || !pv) return mccsInternalError;
+      const ArenaLayout& L = c->layout;
+      // send connector (to next): poll our head lines, post next's tail lines
+      mccsDevConnInfo& s = peers[next].send[0];
+      s.buffs[MCCS_PROTO_SIMPLE] = sender_local ? me + L.data_off(ch) : nx + L.data_off(ch);
+      s.head = (uint64_t*)(me + L.head_off(ch));
+      s.tail = (uint64_t*)(nx + L.tail_off(ch));
+      // recv connector (from prev): poll our tail lines, post prev's head lines
+      mccsDevConnInfo& r = peers[prev].recv[0];
+      r.buffs[MCCS_PROTO_SIMPLE] = sender_local ? pv + L.data_off(ch) : me + L.data_off(ch);
+      r.tail = (uint64_t*)(me + L.tail_off(ch));
+      r.head = (uint64_t*)(pv + L.head_off(ch));
+    }
+    MCCS_HIP(hipMemcpy(c->d_peers[ch], peers.data(), sizeof(mccsDevChannelPeer) * n, hipMemcpyHostToDevice));
+    MCCS_HIP(hipMemcpy(c->d_user_ranks[ch], user_ranks.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    mccsDevChannel& dc = hc.channels[ch];
+    dc.peers = c->d_peers[ch];
+    dc.ring.prev = prev;
+    dc.ring.next = next;
+    dc.ring.userRanks = c->d_user_ranks[ch];
+    dc.ring.index = (ix_rank + n - ix_zero) % n;
+    dc.workFifoDone = c->d_done + ch;
+  }
+  MCCS_HIP(hipMemcpy(c->d_comm, &hc, sizeof(hc), hipMemcpyHostToDevice));
+  MCCS_CHECK(comm_set_kernel_cfg(c));
+  c->connected = true;
+  return mccsSuccess;
+}
+
+mccsResult_t comm_free(Comm* c) {
+  DeviceGuard g(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (int r = 0; r < (int)c->peer_arena.size(); ++r)
+    if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)hipIpcCloseMemHandle(c->peer_arena[r]);
+  if (c->own_arena) (void)hipFree(c->own_arena);
+  for (auto p : c->d_peers) (void)hipFree(p);
+  for (auto p : c->d_user_ranks) (void)hipFree(p);
+  if (c->d_comm) (void)hipFree(c->d_comm);
+  if (c->d_abort) (void)hipFree(c->d_abort);
+  if (c->h_work) (void)hipHostFree(c->h_work);
+  if (c->h_done) (void)hipHostFree(c->h_done);
+  if (c->event) (void)hipEventDestroy(c->event);
+  if (c->user_event) (void)hipEventDestroy(c->user_event);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  return mccsSuccess;
+}
+
+}  // namespace mccs

@@ -1,0 +1,153 @@
+// comm.h — host runtime of the MI355X mCCS ring path (internal).
+//
+// Mirrors the reference service objects on the hot path:
+//   Communicator ........... src/mccs/src/comm/mod.rs:48-122 (+ proxy/init.rs)
+//   CommDevResources ....... src/mccs/src/comm/device.rs:54-188
+//   ring patterns .......... src/mccs/src/proxy/engine.rs:269-320
+//   KernelPlan / schedule .. src/mccs/src/proxy/plan.rs:40-700
+//   SHM connector .......... src/mccs/src/transport/shm/transporter.rs (replaced
+//                            by an xGMI arena: FIFO data + flag lines in HBM)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "mccs_devcomm.h"
+#include "mccs_hip.h"
+#include "ring_cfg.h"
+
+namespace mccs {
+
+#define MCCS_LOG(...)                        \
+  do {                                       \
+    std::fprintf(stderr, "[mccs] " __VA_ARGS__); \
+    std::fprintf(stderr, "\n");              \
+  } while (0)
+
+// cuda_warning! equivalent (utils/mod.rs:7-26): log, then fail the call.
+#define MCCS_HIP(call)                                                                    \
+  do {                                                                                    \
+    hipError_t _e = (call);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      MCCS_LOG("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(_e));       \
+      return mccsUnhandledCudaError;                                                      \
+    }                                                                                     \
+  } while (0)
+
+#define MCCS_CHECK(call)                  \
+  do {                                    \
+    mccsResult_t _r = (call);             \
+    if (_r != mccsSuccess) return _r;     \
+  } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Per-rank FIFO arena layout (identical on every rank; offsets in bytes).
+// [flags: nch x {send head lines, recv tail lines}] [data: nch x buffer_size]
+struct ArenaLayout {
+  int nch = 0;
+  size_t buffer_size = 0;
+  static constexpr size_t kLinesBytes = (size_t)MCCS_MAX_LANES * MCCS_FLAG_LINE_BYTES;  // 2 KiB
+  size_t head_off(int c) const { return (size_t)c * 2 * kLinesBytes; }
+  size_t tail_off(int c) const { return (size_t)c * 2 * kLinesBytes + kLinesBytes; }
+  size_t flags_bytes() const { return (((size_t)nch * 2 * kLinesBytes) + 65535) & ~(size_t)65535; }
+  size_t data_off(int c) const { return flags_bytes() + (size_t)c * buffer_size; }
+  size_t total() const { return flags_bytes() + (size_t)nch * buffer_size; }
+};
+
+// Connect handle exchanged between processes (fixed size, POD).
+struct ConnectHandle {
+  uint32_t magic;
+  int32_t rank, nranks, device;
+  int32_t pid;
+  int32_t fifo_memory;
+  int32_t nch;
+  int32_t pad;
+  uint64_t arena_bytes;
+  uint64_t buffer_size;
+  hipIpcMemHandle_t ipc;
+  char host[64];
+};
+constexpr uint32_t kHandleMagic = 0x6d636373;  // "mccs"
+
+struct WorkElemHost {
+  uint8_t nWarps;
+  const void* send;
+  void* recv;
+  size_t count;
+  uint8_t bid, nChannels;
+};
+
+struct ChannelSchedule {  // plan.rs ChanWorkSchedule
+  size_t coll_bytes = 0;
+  std::vector<std::vector<WorkElemHost>> works;  // KernelWork list
+  std::vector<int> work_func;                   // func id per work (for batching)
+};
+
+struct Comm {
+  int rank = 0, nranks = 1, device = 0;
+  mccsCommConfig cfg{};
+  int nch = 0, lanes = 1, block_threads = 512;
+  std::vector<std::vector<int>> rings;  // per channel send order
+  ArenaLayout layout;
+  // arena: own + mapped peers (index by rank); own_arena is peer_arena[rank]
+  char* own_arena = nullptr;
+  bool own_arena_uncached = true;
+  std::vector<char*> peer_arena;
+  std::vector<bool> peer_opened_ipc;
+  bool all_uncached = true;
+  // device resources (comm/device.rs)
+  mccsDevCommAndChannels* d_comm = nullptr;
+  std::vector<mccsDevChannelPeer*> d_peers;
+  std::vector<int*> d_user_ranks;
+  uint32_t* d_abort = nullptr;
+  // host-mapped work FIFO (comm/mod.rs MCCS_WORK_FIFO_DEPTH) + done counters
+  mccsDevWork* h_work = nullptr;
+  mccsDevWork* d_work = nullptr;
+  uint32_t* h_done = nullptr;
+  uint32_t* d_done = nullptr;
+  uint32_t work_depth = 4096;
+  uint32_t work_next = 0;      // work_queue_next_available
+  uint32_t work_acked_min = 0; // work_queue_acked_min
+  std::vector<uint32_t> chan_next;  // per channel work_queue_next_available
+  hipStream_t stream = nullptr;
+  hipEvent_t event = nullptr;       // comm -> user
+  hipEvent_t user_event = nullptr;  // user -> comm
+  bool connected = false;
+  bool failed = false;
+  // plan state
+  std::vector<ChannelSchedule> sched;
+  int plan_func = -1, plan_dtype = -1, plan_op = -1, plan_threads = 0;
+  bool plan_pending = false;
+};
+
+// comm.cpp
+mccsResult_t comm_alloc_local(Comm* c);
+mccsResult_t comm_build_device(Comm* c);
+void default_rings(int nranks, int nch_req, std::vector<std::vector<int>>* rings);
+mccsResult_t comm_free(Comm* c);
+mccsResult_t comm_set_kernel_cfg(Comm* c);
+// plan.cpp
+mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count);
+mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams);
+// ring.hip
+const void* ring_kernel_ptr(int func, int dtype, int op);
+const void* ring_multi_kernel_ptr(int func, int dtype, int op);
+hipError_t ring_set_device_cfg(const mccsRingKernelCfg& cfg);
+hipError_t ring_take_device_error(unsigned* err);
+
+}  // namespace mccs

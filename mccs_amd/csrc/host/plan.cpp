@@ -1,0 +1,261 @@
+// plan.cpp — kernel plans: task schema, per-channel work elements, the
+// host-mapped work FIFO and the launch (reference src/mccs/src/proxy/plan.rs).
+//
+//   get_task_schema ........ plan.rs:602-635   -> task_schema()
+//   compute_coll_work ...... plan.rs:172-289   -> plan_enqueue()
+//   select_best_channels ... plan.rs:292-302   -> select_channels()
+//   enqueue_work_elem_coll . plan.rs:68-90     -> enqueue_elem()
+//   wait_work_queue ........ plan.rs:380-422   -> wait_work_queue()
+//   upload_work ............ plan.rs:424-541   -> upload_work()
+//   work_elem_conversion ... plan.rs:550-600   -> to_dev_work()
+//   launch_plan ............ plan.rs:638-669   -> plan_launch_group()
+// MI355X differences: the grid is (#channels x lanes) workgroups of
+// cfg.block_threads (the reference launches one block of nWarps*32 per
+// channel); nWarps in each work element keeps the reference value because the
+// kernel's chunk arithmetic (all_reduce.h:30-36) depends on it.
+#include <hip/hip_runtime.h>
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <map>
+
+#include "comm.h"
+#include "dtypes.h"
+
+namespace mccs {
+
+static constexpr int kMaxElemsPerWork = MCCS_MAX_WORK_ELEMENTS;
+static constexpr size_t kSimpleMaxThreads = 512;
+static constexpr size_t kSimpleThreadThreshold = 64;
+
+void task_schema(size_t total_bytes, int nch_cfg, int* nch_out, int* nthreads_out) {
+  size_t nch = (size_t)nch_cfg, nthr = kSimpleMaxThreads;
+  while (total_bytes < nch * nthr * kSimpleThreadThreshold) {
+    if (nch >= 2) nch -= 1;
+    else if (nthr % 128 == 0) nthr /= 2;
+    else break;
+  }
+  nthr += WARP_SIZE;
+  if (nthr / WARP_SIZE < 3) nthr = WARP_SIZE * 3;
+  *nch_out = (int)nch;
+  *nthreads_out = (int)nthr;
+}
+
+static inline bool rolling_less_u32(uint32_t a, uint32_t b) { return (uint32_t)(a - b) > 0x7fffffffu; }
+static inline uint32_t rolling_min_u32(uint32_t a, uint32_t b) { return (uint32_t)(b - a) <= 0x7fffffffu ? a : b; }
+
+// k least-loaded channels, ties by id (ChannelLoad ordering, plan.rs:673-692)
+static std::vector<int> select_channels(const Comm* c, int k) {
+  std::vector<int> ids(c->nch);
+  for (int i = 0; i < c->nch; ++i) ids[i] = i;
+  std::stable_sort(ids.begin(), ids.end(),
+                   [&](int a, int b) { return c->sched[a].coll_bytes < c->sched[b].coll_bytes; });
+  ids.resize(std::min(k, c->nch));
+  return ids;
+}
+
+static void enqueue_elem(ChannelSchedule& s, const WorkElemHost& e, int func_index, size_t esize) {
+  s.coll_bytes += e.count * esize;
+  if (!s.works.empty()) {
+    auto& tail = s.works.back();
+    if (s.work_func.back() == func_index && tail[0].nWarps == e.nWarps && (int)tail.size() < kMaxElemsPerWork) {
+      tail.push_back(e);
+      return;
+    }
+  }
+  s.works.push_back({e});
+  s.work_func.push_back(func_index);
+}
+
+mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count) {
+  if (c->plan_pending && (c->plan_func != func || c->plan_dtype != dtype || c->plan_op != op))
+    return mccsInvalidUsage;  // pre_launch_schedule batches same func/dtype/op only (plan.rs:122-141)
+  const size_t esize = (size_t)elem_bytes(dtype);
+  const size_t total = func == mccsFuncAllGather ? count * c->nranks : count * esize;  // task.rs:95-102
+  int nch = 0, nthr = 0;
+  task_schema(total, c->nch, &nch, &nthr);
+  const std::vector<int> chans = select_channels(c, nch);
+  for (int bid = 0; bid < (int)chans.size(); ++bid) {
+    WorkElemHost e{};
+    e.nWarps = (uint8_t)(nthr / WARP_SIZE);
+    e.send = send;
+    e.recv = recv;
+    e.count = count;
+    e.bid = (uint8_t)bid;
+    e.nChannels = (uint8_t)chans.size();
+    enqueue_elem(c->sched[chans[bid]], e, /*funcIndex, unused (plan.rs:585)*/ 0,
+                 func == mccsFuncAllGather ? 1 : esize);
+  }
+  c->plan_pending = true;
+  c->plan_func = func;
+  c->plan_dtype = dtype;
+  c->plan_op = op;
+  return mccsSuccess;
+}
+
+static mccsDevWork to_dev_work(const std::vector<WorkElemHost>& elems, bool in_fifo, bool is_last, uint32_t u) {
+  mccsDevWork w;
+  std::memset(&w, 0, sizeof(w));
+  for (size_t i = 0; i < elems.size(); ++i) {
+    mccsDevWorkElem& d = w.elems[i];
+    d.isUsed = 1;
+    d.nWarps = elems[i].nWarps;
+    d.sendbuff = elems[i].send;
+    d.recvbuff = elems[i].recv;
+    d.count = elems[i].count;
+    d.root = 0;
+    d.bid = elems[i].bid;
+    d.nChannels = elems[i].nChannels;
+    d.redOpArg = 0;
+  }
+  w.header.funcIndex = 0;
+  w.header.type = mccsDevWorkTypeColl;
+  w.header.inFifo = in_fifo ? 1 : 0;
+  w.header.isLast = is_last ? 1 : 0;
+  if (is_last) w.header.doneAcks = u;
+  else w.header.workNext = (int32_t)u;
+  return w;
+}
+
+static mccsResult_t wait_work_queue(Comm* c, uint32_t target) {
+  if (!rolling_less_u32(c->work_acked_min + c->work_depth, target)) return mccsSuccess;
+  for (uint64_t spins = 0;; ++spins) {
+    uint32_t ackd[MCCS_MAX_NCHANNELS];
+    for (int i = 0; i < MCCS_MAX_NCHANNELS; ++i) ackd[i] = __atomic_load_n(&c->h_done[i], __ATOMIC_RELAXED);
+    uint32_t all = c->work_next;
+    for (int ch = 0; ch < c->nch; ++ch)
+      if (ackd[ch] != c->chan_next[ch]) all = rolling_min_u32(all, ackd[ch]);
+    for (int ch = 0; ch < c->nch; ++ch)
+      if (ackd[ch] == c->chan_next[ch]) __atomic_store_n(&c->h_done[ch], all, __ATOMIC_RELAXED);
+    c->work_acked_min = all;
+    if (!rolling_less_u32(c->work_acked_min + c->work_depth, target)) return mccsSuccess;
+    if ((spins & 0xfffff) == 0xfffff && hipStreamQuery(c->stream) == hipSuccess) {
+      // stream idle but acks missing: the kernel aborted
+      return mccsRemoteError;
+    }
+    sched_yield();
+  }
+}
+
+struct LaunchDesc {
+  const void* fn = nullptr;
+  const void* multi_fn = nullptr;
+  uint64_t mask = 0;
+  int nch_used = 0;
+  mccsDevWork* work = nullptr;
+};
+
+static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
+  std::vector<int> chan_list;
+  uint64_t mask = 0;
+  uint32_t work_count = 0;
+  for (int ch = 0; ch < c->nch; ++ch)
+    if (!c->sched[ch].works.empty()) {
+      chan_list.push_back(ch);
+      mask |= 1ull << ch;
+      work_count += (uint32_t)c->sched[ch].works.size();
+    }
+  if (chan_list.empty()) return mccsInternalError;
+  const uint32_t qmask = c->work_depth - 1;
+  const uint32_t nchan = (uint32_t)chan_list.size();
+  uint32_t first = c->work_next;
+  if (((first + nchan - 1) & qmask) < (first & qmask)) {  // wrap: restart at slot 0
+    first = (first + qmask) & ~qmask;
+    c->work_next = first;
+  }
+  MCCS_CHECK(wait_work_queue(c, first + work_count));
+  uint32_t subsequent = first + nchan;
+  for (uint32_t nth = 0; nth < nchan; ++nth) {
+    const int ch = chan_list[nth];
+    auto& works = c->sched[ch].works;
+    for (size_t wid = 0; wid < works.size(); ++wid) {
+      mccsDevWork dw;
+      if (wid == works.size() - 1) {
+        c->chan_next[ch] = subsequent + 1;
+        dw = to_dev_work(works[wid], true, true, subsequent + 1);
+      } else {
+        const uint32_t nxt = (wid == 0 ? subsequent : subsequent + 1) & qmask;
+        dw = to_dev_work(works[wid], false, false, (uint32_t)((int32_t)nxt - (int32_t)(first & qmask)));
+      }
+      uint32_t cur;
+      if (wid == 0) {
+        cur = first + nth;
+      } else {
+        cur = subsequent;
+        subsequent += 1;
+      }
+      c->h_work[cur & qmask] = dw;
+    }
+  }
+  c->work_next = subsequent;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  ld->mask = mask;
+  ld->nch_used = (int)nchan;
+  ld->work = c->d_work + (first & qmask);
+  ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
+  ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
+  for (auto& s : c->sched) s = ChannelSchedule{};
+  c->plan_pending = false;
+  return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
+}
+
+// Launch every pending plan.  Comms on distinct devices get one launch each
+// (on their own stream, bridged to the caller's stream with events like
+// libmccs: collectives.rs:86,134 + proxy/engine.rs:1185-1189); comms sharing a
+// device are fused into one multi-rank launch so their ring blocks are
+// co-resident (they spin on each other's flags).
+mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams) {
+  std::map<int, std::vector<int>> by_dev;
+  for (int i = 0; i < (int)comms.size(); ++i)
+    if (comms[i]->plan_pending) by_dev[comms[i]->device].push_back(i);
+  for (auto& kv : by_dev) {
+    const std::vector<int>& idx = kv.second;
+    DeviceGuard g(kv.first);
+    std::vector<LaunchDesc> lds(idx.size());
+    for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work(comms[idx[k]], &lds[k]));
+    Comm* c0 = comms[idx[0]];
+    const bool bridge = c0->cfg.bridge_streams >= 0;
+    hipStream_t st = bridge ? c0->stream : user_streams[idx[0]];
+    if (bridge || idx.size() > 1) {
+      for (size_t k = 0; k < idx.size(); ++k) {
+        Comm* c = comms[idx[k]];
+        MCCS_HIP(hipEventRecord(c->user_event, user_streams[idx[k]]));
+        MCCS_HIP(hipStreamWaitEvent(st, c->user_event, 0));
+      }
+    }
+    const unsigned grid = (unsigned)(lds[0].nch_used * c0->lanes);
+    const unsigned block = (unsigned)c0->block_threads;
+    if (idx.size() == 1) {
+      mccsDevComm* dcomm = (mccsDevComm*)c0->d_comm;
+      void* args[3] = {&dcomm, &lds[0].mask, &lds[0].work};
+      MCCS_HIP(hipLaunchKernel(lds[0].fn, dim3(grid), dim3(block), args, 0, st));
+    } else {
+      if (idx.size() > MCCS_MULTI_MAX_RANKS) return mccsInvalidUsage;
+      mccsMultiLaunchArgs ma;
+      std::memset(&ma, 0, sizeof(ma));
+      ma.channelMask = lds[0].mask;
+      for (size_t k = 0; k < idx.size(); ++k) {
+        if (lds[k].mask != lds[0].mask || lds[k].multi_fn != lds[0].multi_fn ||
+            comms[idx[k]]->lanes != c0->lanes || comms[idx[k]]->block_threads != c0->block_threads)
+          return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
+        ma.comm[k] = (mccsDevComm*)comms[idx[k]]->d_comm;
+        ma.work[k] = lds[k].work;
+      }
+      void* args[1] = {&ma};
+      MCCS_HIP(hipLaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, 0, st));
+    }
+    MCCS_HIP(hipEventRecord(c0->event, st));
+    if (bridge || idx.size() > 1) {
+      for (size_t k = 0; k < idx.size(); ++k) {
+        if (!bridge && k == 0) continue;
+        MCCS_HIP(hipStreamWaitEvent(user_streams[idx[k]], c0->event, 0));
+      }
+    }
+    for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(hipEventRecord(comms[idx[k]]->event, st));
+  }
+  return mccsSuccess;
+}
+
+}  // namespace mccs

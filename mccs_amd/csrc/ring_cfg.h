@@ -1,0 +1,39 @@
+// ring_cfg.h — conventions shared by the ring kernels and the C++ host.
+//
+// FIFO flag lines.  A connector's `tail` / `head` pointers (mccsDevConnInfo,
+// devcomm.h:36-46) point at an array of 128-byte lines, one per lane (a lane
+// is one workgroup of a channel; the reference has exactly one, lane 0):
+//   word 0  the step counter the peer polls / we poll
+//   word 1  this side's saved step for the lane (local lines only)
+// With one lane this is binary-compatible with the reference SHM metadata
+// (SendBufMeta.head / RecvBufMeta.tail at offset 0 followed by 120 pad bytes,
+// src/mccs/src/transport/meta.rs:7-67), so word 1 is free padding there.
+#pragma once
+#include <stdint.h>
+
+#define MCCS_FLAG_LINE_BYTES 128
+#define MCCS_FLAG_LINE_WORDS (MCCS_FLAG_LINE_BYTES / 8)
+#define MCCS_MAX_LANES 16
+
+// Fence policy for FIFO hand-offs (device global, per device; set by the host).
+#define MCCS_FENCE_SYSTEM 0   // FIFO memory may be cached: system-scope release/acquire
+#define MCCS_FENCE_UNCACHED 1 // FIFO memory is uncached (hipDeviceMallocUncached): drains only
+
+// Error bits reported through the device-global error word.
+#define MCCS_ERR_TIMEOUT 1u
+#define MCCS_ERR_ABORTED 2u
+
+struct mccsRingKernelCfg {
+  uint32_t fence_mode;    // MCCS_FENCE_*
+  uint32_t pad;
+  uint64_t timeout_ticks; // s_memrealtime ticks (100 MHz); 0 = never
+};
+
+// Multi-rank launch (several communicators of one device in ONE launch, used
+// when ranks share a GPU: tests' virtual node).  blockIdx.y = rank slot.
+#define MCCS_MULTI_MAX_RANKS 16
+struct mccsMultiLaunchArgs {
+  struct mccsDevComm* comm[MCCS_MULTI_MAX_RANKS];
+  struct mccsDevWork* work[MCCS_MULTI_MAX_RANKS];
+  uint64_t channelMask;
+};

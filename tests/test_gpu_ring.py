@@ -1,0 +1,233 @@
+"""GPU parity of the ring AllReduce / AllGather path against the oracle.
+
+Runs an n-rank virtual node on one MI355X (tests/vnode.py): the production
+kernels, FIFO protocol, work list and planner, with all ranks' FIFOs in one
+GPU's HBM.  Integer and exact-sum inputs are checked against arithmetic
+known answers (allreduce_proto main.rs:111); fp inputs bit for bit against
+the oracle's ring-order restatement (all_reduce.h summation order, per-hop
+rounding in T).  Every rank's output must be identical.
+"""
+import numpy as np
+import pytest
+
+from mccs_amd import comm as C
+import vnode
+
+pytestmark = pytest.mark.gpu
+
+F16, F32, BF16, I32, F64, I8 = 6, 7, 9, 2, 8, 0
+
+
+def _check_all_equal(outs, exp, code):
+    for r, o in enumerate(outs):
+        assert np.array_equal(o.view(np.uint8), exp.view(np.uint8)), f"rank {r} differs from oracle"
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("code", [F32, F16, BF16])
+def test_allreduce_matches_oracle(orc, n, code):
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(n * 10 + code)
+        inputs = [vnode.gen(code, 300007, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, code, 0)
+        exp = vnode.expected_allreduce(orc, inputs, code, 0, comms[0])
+        _check_all_equal(outs, exp, code)
+    finally:
+        vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_allreduce_proto_kat(n):
+    """allreduce_proto: int32 Sum, rank r holds 2042+r (scaled to 2 ring loops + tail)."""
+    comms = C.init_all([0] * n)
+    try:
+        count = 2 * comms[0].nchannels * n * (1 << 20) // 4 + 999
+        inputs = [np.full(count, 2042 + r, dtype=np.int32) for r in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, I32, 0)
+        for o in outs:
+            assert np.all(o == 2042 * n + n * (n - 1) // 2)
+    finally:
+        vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("code", [F16, F32])
+def test_exact_sum_inputs(n, code):
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(77)
+        ks = [rng.integers(-255, 256, 200001) for _ in range(n)]
+        inputs = [(k / 64.0).astype(vnode.NPDT[code]) for k in ks]
+        outs = vnode.run_allreduce(comms, inputs, code, 0)
+        exact = np.sum(np.stack(ks), axis=0) / 64.0
+        for o in outs:
+            assert np.array_equal(o.astype(np.float64), exact)
+    finally:
+        vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("op", [1, 2, 3])
+@pytest.mark.parametrize("code", [F32, F16, I32])
+def test_allreduce_ops(orc, op, code):
+    n = 4
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(op)
+        inputs = [vnode.gen(code, 65537, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, code, op)
+        exp = vnode.expected_allreduce(orc, inputs, code, op, comms[0])
+        _check_all_equal(outs, exp, code)
+    finally:
+        vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("count", [1, 7, 255, 256, 4097, 1 << 20, 5 * (1 << 19) // 2 + 77, (3 << 20) + 5])
+def test_allreduce_sizes(orc, count):
+    n = 4
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(count)
+        inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, F16, 0)
+        exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0])
+        _check_all_equal(outs, exp, F16)
+    finally:
+        vnode.destroy(comms)
+
+
+def test_allreduce_in_place(orc):
+    n = 8
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(5)
+        inputs = [vnode.gen(F32, 1 << 21, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, F32, 0, inplace=True)
+        exp = vnode.expected_allreduce(orc, inputs, F32, 0, comms[0])
+        _check_all_equal(outs, exp, F32)
+    finally:
+        vnode.destroy(comms)
+
+
+def test_repeated_calls_keep_fifo_steps(orc):
+    """conn->step persists across launches (prims_simple.h:318-319,461)."""
+    n = 4
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(9)
+        for it, count in enumerate([100003, 7, 1 << 20, 33, 250001]):
+            inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
+            outs = vnode.run_allreduce(comms, inputs, F16, 0)
+            exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0])
+            _check_all_equal(outs, exp, F16)
+    finally:
+        vnode.destroy(comms)
+
+
+def test_group_batches_and_chains_works(orc):
+    """12 allreduces in one group: >10 elements per channel forces a second
+    mccsDevWork chained by workNext (plan.rs:68-90, 424-541; common.h:151-178)."""
+    n = 4
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(12)
+        counts = [1000 + 7919 * i for i in range(12)]
+        ins = [[vnode.gen(F32, cnt, rng) for _ in range(n)] for cnt in counts]
+        sends = [[vnode.to_dev(x) for x in per] for per in ins]
+        recvs = [[vnode.to_dev(np.zeros_like(x)) for x in per] for per in ins]
+        with C.group():
+            for k, cnt in enumerate(counts):
+                for r in range(n):
+                    C.all_reduce(comms[r], sends[k][r], recvs[k][r], cnt, F32, 0)
+        for c in comms:
+            c.sync()
+        planner = vnode.Planner(comms[0].nchannels, comms[0].rings())
+        for k, cnt in enumerate(counts):
+            exp = vnode.expected_allreduce(orc, ins[k], F32, 0, comms[0], planner=planner)
+            for r in range(n):
+                got = vnode.from_dev(recvs[k][r], F32)
+                assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), (k, r)
+    finally:
+        vnode.destroy(comms)
+
+
+CONFIGS = [
+    dict(lanes=1),
+    dict(lanes=3),
+    dict(lanes=8, block_threads=256),
+    dict(block_threads=1024),
+    dict(locality=C.LOCALITY_RECEIVER),
+    dict(fifo_memory=C.FIFO_DEVICE),
+    dict(buffer_size=1 << 20),
+    dict(channel_count=2, rings="default", block_threads=544, lanes=1),  # reference profile
+    dict(channel_count=5),
+    dict(bridge_streams=-1),
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[str(c) for c in CONFIGS])
+def test_configs(orc, cfg):
+    n = 8
+    cfg = dict(cfg)
+    if cfg.get("rings") == "default":
+        cfg["rings"] = [list(range(n))] * cfg["channel_count"]
+    comms = C.init_all([0] * n, C.CommConfig(**cfg))
+    try:
+        rng = np.random.default_rng(len(str(cfg)))
+        inputs = [vnode.gen(F16, 777777, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, F16, 0)
+        exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0], buff_size=cfg.get("buffer_size", 1 << 22))
+        _check_all_equal(outs, exp, F16)
+    finally:
+        vnode.destroy(comms)
+
+
+def test_single_rank_is_copy():
+    import torch
+
+    (c,) = C.init_all([0])
+    try:
+        x = torch.arange(1000, dtype=torch.float32, device="cuda")
+        y = torch.zeros_like(x)
+        C.all_reduce(c, x, y, 1000, C.AllReduceDataType.Float32)
+        c.sync()
+        assert torch.equal(x, y)
+    finally:
+        vnode.destroy([c])
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("nbytes", [1, 1000, 1 << 20, (5 << 20) + 3])
+def test_allgather(orc, n, nbytes):
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(nbytes)
+        inputs = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(n)]
+        send = [vnode.to_dev(x) for x in inputs]
+        recv = [vnode.to_dev(np.zeros(n * nbytes, np.uint8)) for _ in range(n)]
+        with C.group():
+            for r in range(n):
+                C.all_gather(comms[r], send[r], recv[r], nbytes)
+        for c in comms:
+            c.sync()
+        exp = orc.ring_allgather(inputs)
+        for r in range(n):
+            assert np.array_equal(recv[r].cpu().numpy(), exp), r
+    finally:
+        vnode.destroy(comms)
+
+
+def test_bad_usage_fails_loudly():
+    comms = C.init_all([0, 0])
+    try:
+        import torch
+
+        x = torch.zeros(16, device="cuda")
+        with pytest.raises(Exception):
+            C.all_reduce(comms[0], x, x, 16, 42)  # bad dtype
+        with pytest.raises(Exception):
+            with C.group():
+                C.all_reduce(comms[0], x, x, 16, C.AllReduceDataType.Float32)
+                C.all_reduce(comms[0], x, x, 16, C.AllReduceDataType.Float16)  # mixed plan
+    finally:
+        vnode.destroy(comms)
