@@ -23,6 +23,7 @@ struct GroupState {
   std::vector<Comm*> comms;
   std::vector<hipStream_t> streams;
 };
+static thread_local GroupState g_group;
 
 // Drops every plan queued in the current group (error path).
 static void group_discard() {
@@ -33,7 +34,6 @@ static void group_discard() {
   g_group.comms.clear();
   g_group.streams.clear();
 }
-static thread_local GroupState g_group;
 
 static void fill_defaults(mccsCommConfig* c) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
