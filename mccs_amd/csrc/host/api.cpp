@@ -90,6 +90,14 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   c->nch = (int)c->rings.size();
   c->block_threads = cfg.block_threads;
   c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, 16 / c->nch)));
+  // every lane owns a >= 256-byte region of each 2-step slot pair (ring.hip)
+  while (c->lanes > 1 && (size_t)cfg.buffer_size / MCCS_BUFFER_SLOTS * 2 / c->lanes < 256) {
+    if (cfg.lanes > 0) {
+      delete c;
+      return mccsInvalidArgument;
+    }
+    c->lanes /= 2;
+  }
   *out = c;
   return mccsSuccess;
 }
@@ -199,13 +207,7 @@ extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks,
       // IPC export of the uncached arena refused: fall back to a plain device arena
       MCCS_LOG("hipIpcGetMemHandle(uncached arena): %s; retrying with hipMalloc", hipGetErrorString(e));
       (void)hipGetLastError();
-      (void)hipFree(c->own_arena);
-      c->own_arena = nullptr;
-      c->own_arena_uncached = false;
-      e = hipMalloc((void**)&c->own_arena, c->layout.total());
-      if (e == hipSuccess) e = hipMemset(c->own_arena, 0, c->layout.total());
-      if (e == hipSuccess) e = hipIpcGetMemHandle(&h.ipc, c->own_arena);
-      c->peer_arena[rank] = c->own_arena;
+      if (comm_switch_to_device_arena(c) == mccsSuccess) e = hipIpcGetMemHandle(&h.ipc, c->own_arena);
     }
     if (e != hipSuccess) {
       MCCS_LOG("hipIpcGetMemHandle: %s", hipGetErrorString(e));

@@ -13,8 +13,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <mutex>
 
 #include "comm.h"
 
@@ -90,6 +92,53 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
   return mccsSuccess;
 }
 
+// Process-wide FIFO arena pool.  Arenas are never returned to the runtime:
+// on this ROCm stack a virtual range freed as one memory type (coarse device
+// memory) and re-allocated as another (uncached) kept behaving like the old
+// type inside kernels (stale translations), corrupting FIFO hand-offs.
+// Pooling by (device, type, size) means the library never flips the type of
+// a range it owns.
+struct PooledArena {
+  int device;
+  bool uncached;
+  size_t bytes;
+  char* ptr;
+};
+static std::mutex g_pool_mu;
+static std::vector<PooledArena> g_pool;
+
+static char* pool_take(int device, bool uncached, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (size_t i = 0; i < g_pool.size(); ++i)
+    if (g_pool[i].device == device && g_pool[i].uncached == uncached && g_pool[i].bytes == bytes) {
+      char* p = g_pool[i].ptr;
+      g_pool.erase(g_pool.begin() + i);
+      return p;
+    }
+  return nullptr;
+}
+
+static void pool_give(int device, bool uncached, size_t bytes, char* p) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool.push_back(PooledArena{device, uncached, bytes, p});
+}
+
+// Swap this comm's uncached arena for a plain device arena (used when IPC
+// export of the uncached one is refused).  The old range goes back to the pool.
+mccsResult_t comm_switch_to_device_arena(Comm* c) {
+  DeviceGuard g(c->device);
+  const size_t bytes = c->layout.total();
+  if (c->own_arena) pool_give(c->device, c->own_arena_uncached, bytes, c->own_arena);
+  c->own_arena_uncached = false;
+  c->own_arena = pool_take(c->device, false, bytes);
+  if (!c->own_arena) MCCS_HIP(hipMalloc((void**)&c->own_arena, bytes));
+  MCCS_HIP(hipMemset(c->own_arena, 0, bytes));
+  MCCS_HIP(ring_flush_caches(nullptr));
+  MCCS_HIP(hipDeviceSynchronize());
+  c->peer_arena[c->rank] = c->own_arena;
+  return mccsSuccess;
+}
+
 mccsResult_t comm_alloc_local(Comm* c) {
   DeviceGuard g(c->device);
   c->layout.nch = c->nch;
@@ -98,17 +147,42 @@ mccsResult_t comm_alloc_local(Comm* c) {
   c->own_arena = nullptr;
   c->own_arena_uncached = false;
   if (c->cfg.fifo_memory == MCCS_FIFO_UNCACHED) {
-    hipError_t e = hipExtMallocWithFlags((void**)&c->own_arena, bytes, hipDeviceMallocUncached);
-    if (e == hipSuccess) {
+    c->own_arena = pool_take(c->device, true, bytes);
+    if (c->own_arena) {
       c->own_arena_uncached = true;
     } else {
-      (void)hipGetLastError();
-      MCCS_LOG("uncached FIFO arena unavailable (%s); using hipMalloc + system fences", hipGetErrorString(e));
-      c->own_arena = nullptr;
+      hipError_t e = hipExtMallocWithFlags((void**)&c->own_arena, bytes, hipDeviceMallocUncached);
+      if (e == hipSuccess) {
+        c->own_arena_uncached = true;
+      } else {
+        (void)hipGetLastError();
+        MCCS_LOG("uncached FIFO arena unavailable (%s); using hipMalloc + system fences", hipGetErrorString(e));
+        c->own_arena = nullptr;
+      }
     }
   }
-  if (!c->own_arena) MCCS_HIP(hipMalloc((void**)&c->own_arena, bytes));
+  if (!c->own_arena) {
+    c->own_arena = pool_take(c->device, false, bytes);
+    if (!c->own_arena) MCCS_HIP(hipMalloc((void**)&c->own_arena, bytes));
+  }
+  if (c->own_arena_uncached) {
+    // trust but verify: the runtime must report the uncached allocation flag
+    hipPointerAttribute_t attr;
+    std::memset(&attr, 0, sizeof(attr));
+    if (hipPointerGetAttributes(&attr, c->own_arena) != hipSuccess ||
+        attr.allocationFlags != hipDeviceMallocUncached) {
+      (void)hipGetLastError();
+      MCCS_LOG("arena %p reports allocationFlags=0x%x, not uncached: using system fences", (void*)c->own_arena,
+               attr.allocationFlags);
+      c->own_arena_uncached = false;
+    }
+  }
+  if (std::getenv("MCCS_DEBUG"))
+    MCCS_LOG("rank %d arena %p bytes %zu uncached=%d", c->rank, (void*)c->own_arena, bytes,
+             (int)c->own_arena_uncached);
   MCCS_HIP(hipMemset(c->own_arena, 0, bytes));
+  MCCS_HIP(ring_flush_caches(nullptr));
+  MCCS_HIP(hipDeviceSynchronize());
   c->peer_arena.assign(c->nranks, nullptr);
   c->peer_opened_ipc.assign(c->nranks, false);
   c->peer_arena[c->rank] = c->own_arena;
@@ -198,7 +272,7 @@ mccsResult_t comm_free(Comm* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
     if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)hipIpcCloseMemHandle(c->peer_arena[r]);
-  if (c->own_arena) (void)hipFree(c->own_arena);
+  if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->layout.total(), c->own_arena);
   for (auto p : c->d_peers) (void)hipFree(p);
   for (auto p : c->d_user_ranks) (void)hipFree(p);
   if (c->d_comm) (void)hipFree(c->d_comm);

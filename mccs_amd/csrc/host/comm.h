@@ -137,6 +137,7 @@ struct Comm {
 
 // comm.cpp
 mccsResult_t comm_alloc_local(Comm* c);
+mccsResult_t comm_switch_to_device_arena(Comm* c);
 mccsResult_t comm_build_device(Comm* c);
 void default_rings(int nranks, int nch_req, std::vector<std::vector<int>>* rings);
 mccsResult_t comm_free(Comm* c);
@@ -149,5 +150,6 @@ const void* ring_kernel_ptr(int func, int dtype, int op);
 const void* ring_multi_kernel_ptr(int func, int dtype, int op);
 hipError_t ring_set_device_cfg(const mccsRingKernelCfg& cfg);
 hipError_t ring_take_device_error(unsigned* err);
+hipError_t ring_flush_caches(hipStream_t st);
 
 }  // namespace mccs

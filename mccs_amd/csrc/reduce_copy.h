@@ -29,7 +29,9 @@ __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
 // Runtime nsrcs in [1, MAXS], ndsts in [1, MAXD]. Threads [tid, nthr) of the
 // calling group participate. Used by the ring primitives (one workgroup per
 // channel lane) where nsrcs/ndsts vary per primitive call.
-template <int DT, int OP, int U, int MAXS, int MAXD, int LDPOL = kPlain, int STPOL = kPlain>
+// NTMASK: bit s set -> source s is read with non-temporal loads, which bypass
+// the CU's L1 (used for FIFO slots another workgroup rewrites between reads).
+template <int DT, int OP, int U, int MAXS, int MAXD, int LDPOL = kPlain, int STPOL = kPlain, int NTMASK = 0>
 __device__ __forceinline__ void reduce_copy_group(const void* const* srcs, int nsrcs,
                                                   void* const* dsts, int ndsts, int64_t nelem,
                                                   int tid, int nthr) {
@@ -52,13 +54,16 @@ __device__ __forceinline__ void reduce_copy_group(const void* const* srcs, int n
     for (; p + (int64_t)(U - 1) * nthr < npack; p += step) {
       u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16<LDPOL>((const u32x4*)srcs[0] + p + (int64_t)u * nthr);
+      for (int u = 0; u < U; ++u)
+        v[u] = ld16<(NTMASK & 1) ? kNonTemporal : LDPOL>((const u32x4*)srcs[0] + p + (int64_t)u * nthr);
 #pragma unroll
       for (int s = 1; s < MAXS; ++s) {
         if (s < nsrcs) {
           u32x4 w[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) w[u] = ld16<LDPOL>((const u32x4*)srcs[s] + p + (int64_t)u * nthr);
+          for (int u = 0; u < U; ++u)
+            w[u] = ((NTMASK >> s) & 1) ? ld16<kNonTemporal>((const u32x4*)srcs[s] + p + (int64_t)u * nthr)
+                                       : ld16<LDPOL>((const u32x4*)srcs[s] + p + (int64_t)u * nthr);
 #pragma unroll
           for (int u = 0; u < U; ++u) v[u] = pack_op<DT, OP>(v[u], w[u]);
         }
@@ -73,10 +78,12 @@ __device__ __forceinline__ void reduce_copy_group(const void* const* srcs, int n
     }
     // remainder packs, one at a time
     for (; p < npack; p += nthr) {
-      u32x4 v = ld16<LDPOL>((const u32x4*)srcs[0] + p);
+      u32x4 v = ld16<(NTMASK & 1) ? kNonTemporal : LDPOL>((const u32x4*)srcs[0] + p);
 #pragma unroll
       for (int s = 1; s < MAXS; ++s)
-        if (s < nsrcs) v = pack_op<DT, OP>(v, ld16<LDPOL>((const u32x4*)srcs[s] + p));
+        if (s < nsrcs)
+          v = pack_op<DT, OP>(v, ((NTMASK >> s) & 1) ? ld16<kNonTemporal>((const u32x4*)srcs[s] + p)
+                                                     : ld16<LDPOL>((const u32x4*)srcs[s] + p));
 #pragma unroll
       for (int d = 0; d < MAXD; ++d)
         if (d < ndsts) st16<STPOL>((u32x4*)dsts[d] + p, v);
@@ -85,10 +92,12 @@ __device__ __forceinline__ void reduce_copy_group(const void* const* srcs, int n
   }
   // typed scalar tail / unaligned fallback
   for (int64_t e = done + tid; e < nelem; e += nthr) {
-    T v = ((const T*)srcs[0])[e];
+    T v = (NTMASK & 1) ? __builtin_nontemporal_load((const T*)srcs[0] + e) : ((const T*)srcs[0])[e];
 #pragma unroll
     for (int s = 1; s < MAXS; ++s)
-      if (s < nsrcs) v = scalar_op<DT, OP>(v, ((const T*)srcs[s])[e]);
+      if (s < nsrcs)
+        v = scalar_op<DT, OP>(v, ((NTMASK >> s) & 1) ? __builtin_nontemporal_load((const T*)srcs[s] + e)
+                                                     : ((const T*)srcs[s])[e]);
 #pragma unroll
     for (int d = 0; d < MAXD; ++d)
       if (d < ndsts) ((T*)dsts[d])[e] = v;

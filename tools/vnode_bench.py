@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Virtual-node ring allreduce timing on ONE GPU (all ranks share its HBM).
+
+Not the xGMI number: every rank's FIFO traffic lands in the same HBM, so this
+measures protocol overhead and per-lane streaming, not link bandwidth.
+  python tools/vnode_bench.py [--sizes-mib 128] [--n 2 4 8]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+
+    from mccs_amd import comm as C
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--sizes-mib", type=int, nargs="+", default=[1, 16, 128])
+    ap.add_argument("--lanes", type=int, nargs="+", default=[0])
+    ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    for n in args.n:
+        for lanes in args.lanes:
+            comms = C.init_all([0] * n, C.CommConfig(lanes=lanes, block_threads=args.block))
+            for mib in args.sizes_mib:
+                cnt = (mib << 20) // 4
+                xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
+                ys = [torch.empty_like(x) for x in xs]
+
+                def once():
+                    with C.group():
+                        for r in range(n):
+                            C.all_reduce(comms[r], xs[r], ys[r], cnt, C.AllReduceDataType.Float32)
+
+                once()
+                for c in comms:
+                    c.sync()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.iters):
+                    once()
+                for c in comms:
+                    c.sync()
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / args.iters
+                print(json.dumps({"n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels,
+                                  "block": comms[0].block_threads, "MiB": mib, "ms": round(dt * 1e3, 3),
+                                  "algbw_GBps": round((mib << 20) / dt / 1e9, 2)}), flush=True)
+                del xs, ys
+            torch.cuda.synchronize()
+            for c in comms:
+                c.destroy()
+
+
+if __name__ == "__main__":
+    main()
