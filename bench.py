@@ -275,8 +275,24 @@ def sweep_variants(sets, n, code, stream):
     mccs_amd.tune()
 
 
+def relaunch_under_torchrun(args) -> int:
+    """`python bench.py --gpus N` outside torchrun: start N ranks as children
+    (this process has not touched the GPU) and return their exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_under_torchrun(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1:
         from mccs_amd import ring_bench

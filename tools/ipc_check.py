@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Multi-process (one rank per process) parity check through IPC-mapped FIFOs.
+
+  python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29511 tools/ipc_check.py [--device-mod N]
+
+Every rank opens its peers' FIFO arenas with hipIpcOpenMemHandle (the
+multi-GPU bench path).  On a one-GPU box all ranks share cuda:0, which still
+exercises IPC export/open, the two-phase connect and cross-process flag
+hand-offs.  Results are checked against the C oracle (rank 0 gathers inputs).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    from mccs_amd import comm as C
+    from oracle import oracle as orc
+    import vnode
+
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    dev = int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def exchange(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+
+    results = {}
+    for mode, fifo in (("uncached", C.FIFO_UNCACHED), ("device", C.FIFO_DEVICE)):
+        comm = C.init_communicator_rank(rank, world, dev, exchange,
+                                        C.CommConfig(fifo_memory=fifo, timeout_ms=20000))
+        for code, count in ((2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)):
+            rng = np.random.default_rng(count * 31 + rank)
+            x = vnode.gen(code, count, rng)
+            if code == 2:
+                x = np.full(count, 2042 + rank, np.int32)
+            xs = [None] * world
+            dist.all_gather_object(xs, x)
+            send = vnode.to_dev(x)
+            recv = vnode.to_dev(np.zeros_like(x))
+            ok = True
+            try:
+                C.all_reduce(comm, send, recv, count, code, 0)
+                comm.sync()
+                got = vnode.from_dev(recv, code)
+                p = vnode.Planner(comm.nchannels, comm.rings())
+                nch, nthr, rings = p.select(count * vnode.ESIZE[code], 0)
+                exp = orc.ring_allreduce(code, 0, xs, nchannels=nch, nthreads=nthr, ring_orders=rings)
+                ok = bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8)))
+            except Exception as e:  # noqa: BLE001
+                print(f"[rank {rank}] {mode} code={code}: {e}", flush=True)
+                ok = False
+            results[f"{mode}/dtype{code}/n{count}"] = ok
+        comm.destroy()
+    allres = [None] * world
+    dist.all_gather_object(allres, results)
+    if rank == 0:
+        merged = {k: all(r[k] for r in allres) for k in results}
+        print(json.dumps({"world": world, "fifo_modes": merged, "all_ok": all(merged.values())}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.exit(0 if all(results.values()) else 1)
+
+
+if __name__ == "__main__":
+    main()
