@@ -147,6 +147,12 @@ mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
 const char *mccsGetErrorString(mccsResult_t r);
 
 /* Host-only helpers (no GPU needed). */
+/* BASELINE configs[0] plumbing: the same ring schedule and FIFO protocol run
+ * by nranks x nchannels host threads over host memory (no GPU).  rings as in
+ * mccsCommConfig (NULL = identity order on every channel). */
+mccsResult_t mccs_host_ring_allreduce(int nranks, const void *const *sendbufs, void *const *recvbufs, size_t count,
+                                      int dtype, int op, int nchannels, int nthreads_ref, int buff_size,
+                                      const int *rings);
 /* Default ring orders for an n-rank node (edge-disjoint Hamiltonian cycles,
  * both directions); writes up to max_channels x nranks ints, returns count. */
 int mccs_default_rings(int nranks, int nch_req, int *out, int max_channels);

@@ -222,6 +222,22 @@ def default_rings(nranks: int, channels: int = 0) -> list[list[int]]:
     return [list(out[c * nranks:(c + 1) * nranks]) for c in range(k)]
 
 
+def host_ring_allreduce(sendbufs, recvbufs, count: int, data_type, op_type=AllReduceOpType.Sum,
+                        channels: int = 1, nthreads: int = 96, buffer_size: int = 1 << 22, rings=None) -> None:
+    """BASELINE configs[0]: the ring protocol on host threads over host memory
+    (numpy arrays or raw host pointers; no GPU)."""
+    n = len(sendbufs)
+    sp = _lib.ptr_array([x.ctypes.data if hasattr(x, "ctypes") else int(x) for x in sendbufs])
+    rp = _lib.ptr_array([x.ctypes.data if hasattr(x, "ctypes") else int(x) for x in recvbufs])
+    ro = None
+    if rings is not None:
+        flat = [int(v) for r in rings for v in r]
+        ro = (_ci * len(flat))(*flat)
+    rc = _sig().mccs_host_ring_allreduce(n, sp, rp, int(count), int(data_type), int(op_type), channels, nthreads,
+                                         buffer_size, ro)
+    _lib.check(rc, "mccs_host_ring_allreduce")
+
+
 def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
     a, b = _ci(), _ci()
     _sig().mccs_task_schema(total_bytes, channels, ctypes.byref(a), ctypes.byref(b))
@@ -230,4 +246,5 @@ def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
 
 __all__ = ["AllReduceDataType", "AllReduceOpType", "CommConfig", "Communicator", "init_all",
            "init_communicator_rank", "all_reduce", "all_gather", "group", "default_rings", "task_schema",
+           "host_ring_allreduce",
            "RedOp", "DataType"]

@@ -43,8 +43,9 @@ static void fill_defaults(mccsCommConfig* c) {
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
-  if (c.buffer_size < 64 * MCCS_BUFFER_SLOTS || c.buffer_size % (256 * MCCS_BUFFER_SLOTS) != 0)
-    return mccsInvalidArgument;
+  // a chunk (buffer_size/2 bytes) must be a multiple of the largest thread
+  // granule (512 x 8 B, all_reduce.h:34-35) so a rounded chunk fits 4 steps
+  if (c.buffer_size < 8192 || c.buffer_size % 8192 != 0) return mccsInvalidArgument;
   // multiples of 32 keep the reference's nWarps*32 blocks (e.g. 544) valid
   if (c.block_threads < 64 || c.block_threads > 1024 || c.block_threads % 32) return mccsInvalidArgument;
   if (c.lanes < 0 || c.lanes > MCCS_MAX_LANES) return mccsInvalidArgument;

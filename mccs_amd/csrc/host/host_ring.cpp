@@ -1,0 +1,283 @@
+// host_ring.cpp — the ring AllReduce protocol run by host threads over host
+// memory: BASELINE configs[0] ("2-rank loopback allreduce, 1 KiB fp32,
+// host-side elementwise sum; plumbing, no GPU").
+//
+// Same protocol as the gfx950 kernels (ring.hip) and the reference
+// (all_reduce.h:10-87 schedule; prims_simple.h:68-237 FIFO: 8 slots, slices of
+// 2 steps, sender waits head + 8 >= step + 2, receiver waits tail >= step + 2,
+// operand order fn(own input, received)), with one std::thread per
+// (rank, channel) and std::atomic head/tail counters.  It exists so the FIFO
+// protocol and schedule can be exercised end to end without a GPU; it is not
+// a fallback for the device path (nothing on the device path calls it).
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "mccs_devcomm.h"
+#include "mccs_hip.h"
+
+namespace {
+
+float h2f(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16, exp = (h >> 10) & 0x1f, man = h & 0x3ffu;
+  uint32_t u;
+  if (exp == 0) {
+    float v = std::ldexp((float)man, -24);
+    return sign ? -v : v;
+  }
+  if (exp == 31) u = sign | 0x7f800000u | (man << 13);
+  else u = sign | ((exp + 112) << 23) | (man << 13);
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+uint16_t f2h(float f) {  // round to nearest even
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u, a = u & 0x7fffffffu;
+  if (a >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0));
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);
+  if (a < 0x38800000u) {
+    float v;
+    std::memcpy(&v, &a, 4);
+    return (uint16_t)(sign | (uint32_t)std::nearbyint(v * 16777216.0f));
+  }
+  uint32_t h = (((a >> 23) - 112) << 10) | ((a & 0x7fffffu) >> 13);
+  const uint32_t rem = a & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h += 1;
+  return (uint16_t)(sign | h);
+}
+
+float b2f(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+uint16_t f2b(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <typename T>
+T iop(int op, T x, T y) {
+  using U = typename std::make_unsigned<T>::type;
+  switch (op) {
+    case mccsDevSum: return (T)((U)x + (U)y);
+    case mccsDevProd: return (T)((U)x * (U)y);
+    case mccsDevMax: return x < y ? y : x;
+    default: return x < y ? x : y;
+  }
+}
+
+template <typename T>
+T fop(int op, T x, T y) {
+  switch (op) {
+    case mccsDevSum: return x + y;
+    case mccsDevProd: return x * y;
+    case mccsDevMax: return x < y ? y : x;
+    default: return x < y ? x : y;
+  }
+}
+
+float hop(int op, float x, float y) {
+  switch (op) {
+    case mccsDevSum: return x + y;
+    case mccsDevProd: return x * y;
+    case mccsDevMax: return std::fmax(x, y);
+    default: return std::fmin(x, y);
+  }
+}
+
+// out[i] = fn(x[i], y[i]); out may alias either input
+void apply(int dt, int op, void* out, const void* x, const void* y, size_t n) {
+#define INT_CASE(D, T)                                                                       \
+  case D:                                                                                    \
+    for (size_t i = 0; i < n; ++i) ((T*)out)[i] = iop<T>(op, ((const T*)x)[i], ((const T*)y)[i]); \
+    break;
+  switch (dt) {
+    INT_CASE(mccsInt8, int8_t)
+    INT_CASE(mccsUint8, uint8_t)
+    INT_CASE(mccsInt32, int32_t)
+    INT_CASE(mccsUint32, uint32_t)
+    INT_CASE(mccsInt64, int64_t)
+    INT_CASE(mccsUint64, uint64_t)
+    case mccsFloat32:
+      for (size_t i = 0; i < n; ++i) ((float*)out)[i] = fop<float>(op, ((const float*)x)[i], ((const float*)y)[i]);
+      break;
+    case mccsFloat64:
+      for (size_t i = 0; i < n; ++i)
+        ((double*)out)[i] = fop<double>(op, ((const double*)x)[i], ((const double*)y)[i]);
+      break;
+    case mccsFloat16:
+      for (size_t i = 0; i < n; ++i)
+        ((uint16_t*)out)[i] = f2h(hop(op, h2f(((const uint16_t*)x)[i]), h2f(((const uint16_t*)y)[i])));
+      break;
+    case mccsBfloat16:
+      for (size_t i = 0; i < n; ++i)
+        ((uint16_t*)out)[i] = f2b(hop(op, b2f(((const uint16_t*)x)[i]), b2f(((const uint16_t*)y)[i])));
+      break;
+  }
+#undef INT_CASE
+}
+
+size_t esize(int dt) {
+  return (dt == mccsInt8 || dt == mccsUint8) ? 1
+         : (dt == mccsFloat16 || dt == mccsBfloat16) ? 2
+         : (dt == mccsInt32 || dt == mccsUint32 || dt == mccsFloat32) ? 4
+         : 8;
+}
+
+struct HostConn {  // one directed FIFO (rank -> next) of one channel
+  std::vector<char> data;
+  std::atomic<uint64_t> head{0}, tail{0};
+};
+
+struct Ctx {
+  int n, nch, dt, op, nthreads_ref, buff_size;
+  size_t es, count;
+  const void* const* send;
+  void* const* recv;
+  const int* rings;  // nch x n, nullptr = identity
+  std::vector<HostConn>* conns;  // [ch * n + rank]: FIFO rank -> next on channel ch
+  std::atomic<int> failed{0};
+  double timeout_s;
+};
+
+// one (rank, channel) thread executing runRing
+void run_rank_channel(Ctx* c, int rank, int ch) {
+  const int n = c->n;
+  std::vector<int> ring(n);
+  for (int i = 0; i < n; ++i) ring[i] = c->rings ? c->rings[ch * n + i] : i;
+  int pos = 0, pos0 = 0;
+  for (int i = 0; i < n; ++i) {
+    if (ring[i] == rank) pos = i;
+    if (ring[i] == 0) pos0 = i;
+  }
+  const int next = ring[(pos + 1) % n], prev = ring[(pos + n - 1) % n];
+  const int ringIx = (pos - pos0 + n) % n;
+  HostConn& out = (*c->conns)[ch * n + rank];
+  HostConn& in = (*c->conns)[ch * n + prev];
+  (void)next;
+  const int64_t stepSize = c->buff_size / MCCS_BUFFER_SLOTS / (int64_t)c->es;
+  const int64_t chunkSize = (int64_t)(int)(stepSize * ALLREDUCE_CHUNKSTEPS);
+  const int64_t size = (int64_t)c->count;
+  const int64_t loopSize = (int64_t)c->nch * n * chunkSize;
+  int64_t gran = (int64_t)(c->nthreads_ref - WARP_SIZE) * 8 / (int64_t)c->es;
+  if (gran < 1) gran = 1;
+  const char* input = (const char*)c->send[rank];
+  char* output = (char*)c->recv[rank];
+  uint64_t rstep = 0, sstep = 0;
+  std::vector<char> tmp((size_t)(2 * stepSize * c->es));
+  const auto t0 = std::chrono::steady_clock::now();
+  auto wait_geq = [&](std::atomic<uint64_t>& f, uint64_t target) {
+    while (f.load(std::memory_order_acquire) < target) {
+      if (c->failed.load(std::memory_order_relaxed)) return false;
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+        c->failed.store(1);
+        return false;
+      }
+      std::this_thread::yield();
+    }
+    return true;
+  };
+  // genericOp: RECV/SEND/SRC(input)/DST(output) flags, two slices per call
+  auto op = [&](bool RECV, bool SEND, bool SRC, bool DST, int64_t srcIx, int64_t dstIx, int64_t nelem) {
+    if (nelem < 0) nelem = 0;
+    int64_t sliceSize = stepSize * ALLREDUCE_SLICESTEPS;
+    const int64_t s = (nelem + 32 - 1) / 32 * 16;
+    sliceSize = s > sliceSize / 32 ? s : sliceSize / 32;
+    int64_t offset = 0;
+    for (int slice = 0; slice < 2; ++slice) {
+      int64_t real = nelem - offset;
+      real = real < sliceSize ? real : sliceSize;
+      if (real < 0) real = 0;
+      if (RECV && !wait_geq(in.tail, rstep + 2)) return false;
+      if (SEND && !wait_geq(out.head, sstep + 2 > 8 ? sstep + 2 - 8 : 0)) return false;
+      const size_t bytes = (size_t)real * c->es;
+      const char* rslot = in.data.data() + (rstep % 8) * stepSize * c->es;
+      char* sslot = out.data.data() + (sstep % 8) * stepSize * c->es;
+      if (bytes) {
+        // vals = srcs[0]; vals = fn(vals, srcs[1]) with srcs = [input?, recv?]
+        if (SRC && RECV) apply(c->dt, c->op, tmp.data(), input + (srcIx + offset) * c->es, rslot, (size_t)real);
+        else if (SRC) std::memcpy(tmp.data(), input + (srcIx + offset) * c->es, bytes);
+        else std::memcpy(tmp.data(), rslot, bytes);
+        if (DST) std::memcpy(output + (dstIx + offset) * c->es, tmp.data(), bytes);
+        if (SEND) std::memcpy(sslot, tmp.data(), bytes);
+      }
+      if (SEND) out.tail.store(sstep + 2, std::memory_order_release);
+      if (RECV) in.head.store(rstep + 2, std::memory_order_release);
+      if (RECV) rstep += 2;
+      if (SEND) sstep += 2;
+      offset += sliceSize;
+    }
+    return true;
+  };
+  auto mod = [&](int r) { return r >= n ? r - n : r; };
+  for (int64_t g = 0; g < size; g += loopSize) {
+    int64_t rcs = (size - g + (int64_t)c->nch * n - 1) / ((int64_t)c->nch * n);
+    rcs = chunkSize < rcs ? chunkSize : rcs;
+    rcs = (int64_t)(int)((rcs + gran - 1) / gran * gran);
+    auto off = [&](int chunk) { return g + (int64_t)ch * n * rcs + (int64_t)chunk * rcs; };
+    auto ne = [&](int64_t o) { return rcs < size - o ? rcs : size - o; };
+    int chunk = mod(ringIx + n - 1);
+    if (!op(false, true, true, false, off(chunk), 0, ne(off(chunk)))) return;
+    for (int j = 2; j < n; ++j) {
+      chunk = mod(ringIx + n - j);
+      if (!op(true, true, true, false, off(chunk), 0, ne(off(chunk)))) return;
+    }
+    chunk = ringIx;
+    if (!op(true, true, true, true, off(chunk), off(chunk), ne(off(chunk)))) return;
+    for (int j = 1; j < n - 1; ++j) {
+      chunk = mod(ringIx + n - j);
+      if (!op(true, true, false, true, 0, off(chunk), ne(off(chunk)))) return;
+    }
+    chunk = mod(ringIx + 1);
+    if (!op(true, false, false, true, 0, off(chunk), ne(off(chunk)))) return;
+  }
+}
+
+}  // namespace
+
+extern "C" mccsResult_t mccs_host_ring_allreduce(int nranks, const void* const* sendbufs, void* const* recvbufs,
+                                                 size_t count, int dtype, int op, int nchannels, int nthreads_ref,
+                                                 int buff_size, const int* rings) {
+  if (nranks < 1 || nranks > 64 || !sendbufs || !recvbufs || dtype < 0 || dtype >= mccsNumTypes || op < 0 ||
+      op > mccsDevMin || nchannels < 1 || nchannels > MCCS_MAX_NCHANNELS || nthreads_ref <= WARP_SIZE ||
+      buff_size < 8192 || buff_size % 8192)
+    return mccsInvalidArgument;
+  const size_t es = esize(dtype);
+  if (nranks == 1) {
+    if (recvbufs[0] != sendbufs[0]) std::memmove(recvbufs[0], sendbufs[0], count * es);
+    return mccsSuccess;
+  }
+  std::vector<HostConn> conns((size_t)nchannels * nranks);
+  for (auto& hc : conns) hc.data.assign((size_t)buff_size, 0);
+  Ctx c;
+  c.n = nranks;
+  c.nch = nchannels;
+  c.dt = dtype;
+  c.op = op;
+  c.nthreads_ref = nthreads_ref;
+  c.buff_size = buff_size;
+  c.es = es;
+  c.count = count;
+  c.send = sendbufs;
+  c.recv = recvbufs;
+  c.rings = rings;
+  c.conns = &conns;
+  c.timeout_s = 60.0;
+  std::vector<std::thread> th;
+  for (int r = 0; r < nranks; ++r)
+    for (int ch = 0; ch < nchannels; ++ch) th.emplace_back(run_rank_channel, &c, r, ch);
+  for (auto& t : th) t.join();
+  return c.failed.load() ? mccsTimeout : mccsSuccess;
+}

@@ -22,12 +22,31 @@ XGMI_LINK_GBPS_PER_DIR = 76.8  # MI355X xGMI per link per direction (spec); see 
 
 
 def _exchange_factory(dist, world):
+    """Connect-handle all-gather over the control plane (replaces the
+    reference's bootstrap ring + exchange engine for this path)."""
     def exchange(b: bytes):
         out = [None] * world
         dist.all_gather_object(out, b)
         return out
 
     return exchange
+
+
+def agree(dist, ok: bool) -> bool:
+    """True only if every rank passed (MIN over ranks)."""
+    import torch
+
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item() == 1)
+
+
+def max_over_ranks(dist, x: float) -> float:
+    import torch
+
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def _exact_inputs(torch, n_elem, rank, dev):
@@ -89,9 +108,7 @@ def run(args):
         except Exception as e:  # noqa: BLE001  (watchdog / HIP error: try the next mode)
             print(f"[rank {rank}] {name}: {e}", flush=True)
             ok = False
-        flags = torch.tensor([1 if ok else 0], dtype=torch.int32)
-        dist.all_reduce(flags, op=dist.ReduceOp.MIN)
-        if flags.item() == 1:
+        if agree(dist, ok):
             mode, validated = name, True
             break
         comm.destroy()
@@ -122,9 +139,7 @@ def run(args):
     comm.sync()
     t1 = time.perf_counter()
     dist.barrier()
-    el = torch.tensor([t1 - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = el.item()
+    elapsed = max_over_ranks(dist, t1 - t0)
     per_step = elapsed / K
     algbw = nbytes / per_step / 1e9
     busbw = algbw * 2 * (world - 1) / world

@@ -301,8 +301,12 @@ int oracle_ring_allreduce(int dtype, int op, int nranks, const void *const *inpu
     in_copy[r] = p;
   }
   c.inputs = in_copy;
-  /* max chunk is buff_size/8*4 bytes */
-  c.tmp = (char *)malloc((size_t)buff_size / 2 + 64);
+  /* largest chunk: buff_size/8*4 bytes rounded up to the thread granule */
+  {
+    size_t gran_b = (size_t)(nthreads_ref > 32 ? nthreads_ref - 32 : 1) * 8;
+    size_t chunk_b = (size_t)buff_size / 2;
+    c.tmp = (char *)malloc((chunk_b + gran_b - 1) / gran_b * gran_b + 64);
+  }
   int rc = c.tmp ? oracle_ring_walk(count, nranks, nchannels, nthreads_ref, buff_size, (int)c.es,
                                     ring_visit, &c)
                  : -2;

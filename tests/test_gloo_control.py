@@ -1,0 +1,105 @@
+"""CPU, world_size 2 over gloo: the N > 1 control plane of bench.py's ring leg
+(connect-handle exchange, all-ranks agreement, max-over-ranks timing) and the
+host ring protocol run per rank with the FIFO messages carried by gloo
+send/recv between processes (sharding + neighbour exchange of the ring)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+
+    from mccs_amd import ring_bench
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ex = ring_bench._exchange_factory(dist, world)
+        got = ex(bytes([rank]) * 8)
+        ok_exchange = got == [bytes([r]) * 8 for r in range(world)]
+        all_true = ring_bench.agree(dist, True)
+        one_false = ring_bench.agree(dist, rank != 1)
+        mx = ring_bench.max_over_ranks(dist, float(rank) + 0.5)
+        # ring allreduce with gloo as the link: rank r holds its chunk sums
+        ring_ok = _gloo_ring_allreduce(dist, rank, world)
+        q.put((rank, ok_exchange, all_true, one_false, mx, ring_ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def _gloo_ring_allreduce(dist, rank, world):
+    """runRing's reduce-scatter + all-gather (all_reduce.h:46-86) with gloo
+    point-to-point as the FIFO; result checked against the C oracle."""
+    import torch
+
+    from oracle import oracle as orc
+
+    rcs = 256  # elements per chunk; count leaves a ragged last chunk
+    count = rcs * world - 5
+    xs = [(np.random.default_rng(100 + r).random(count, dtype=np.float32) * 2 - 1) for r in range(world)]
+    x = torch.from_numpy(xs[rank].copy())
+    out = x.clone()
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+
+    def sl(c):
+        lo = min(c * rcs, count)
+        return slice(lo, min(lo + rcs, count))
+
+    acc = x[sl((rank - 1) % world)].clone()
+    for j in range(2, world + 1):  # reduce-scatter: chunk (rank - j) arrives from prev
+        c = (rank - j) % world
+        buf = torch.empty(sl(c).stop - sl(c).start, dtype=torch.float32)
+        dist.send(acc, nxt) if rank % 2 == 0 else None
+        dist.recv(buf, prv)
+        if rank % 2 == 1:
+            dist.send(acc, nxt)
+        acc = x[sl(c)] + buf  # fn(own input, received)
+    out[sl(rank)] = acc
+    cur = acc
+    for j in range(1, world):  # all-gather
+        c = (rank - j) % world
+        buf = torch.empty(sl(c).stop - sl(c).start, dtype=torch.float32)
+        if rank % 2 == 0:
+            dist.send(cur, nxt)
+            dist.recv(buf, prv)
+        else:
+            dist.recv(buf, prv)
+            dist.send(cur, nxt)
+        out[sl(c)] = buf
+        cur = buf
+    # oracle: 1 channel, 160 threads -> 256-element (1 KiB) granule = rcs
+    exp = orc.ring_allreduce(7, 0, xs, nchannels=1, nthreads=160, buff_size=1 << 22)
+    return bool(np.array_equal(out.numpy().view(np.uint32), exp.view(np.uint32)))
+
+
+@pytest.mark.parametrize("world", [2])
+def test_control_plane_world2(world):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_ex, all_true, one_false, mx, ring_ok in res:
+        assert ok_ex and all_true and not one_false
+        assert mx == world - 0.5
+        assert ring_ok, f"rank {rank}: gloo ring != oracle"
