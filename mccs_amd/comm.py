@@ -64,24 +64,28 @@ FIFO_UNCACHED, FIFO_DEVICE = 0, 1
 
 @dataclass
 class CommConfig:
-    """comm_default_config (mccs.toml:18-20) + MI355X knobs; 0 = library default."""
+    """comm_default_config (mccs.toml:18-20) + MI355X knobs.  None = the
+    library default (mccsCommConfigDefault, which also honours the MCCS_*
+    environment overrides)."""
 
-    channel_count: int = 0
-    buffer_size: int = 0
-    lanes: int = 0
-    block_threads: int = 0
-    locality: int = LOCALITY_SENDER
-    fifo_memory: int = FIFO_UNCACHED
-    timeout_ms: int = 0
-    work_fifo_depth: int = 0
-    bridge_streams: int = 1
+    channel_count: int | None = None
+    buffer_size: int | None = None
+    lanes: int | None = None
+    block_threads: int | None = None
+    locality: int | None = None
+    fifo_memory: int | None = None
+    timeout_ms: int | None = None
+    work_fifo_depth: int | None = None
+    bridge_streams: int | None = None
     rings: list | None = None  # comm_patterns_override: channel_count x nranks send orders
 
     def to_c(self, nranks: int):
         c = _CommConfig()
+        _lib.load().mccsCommConfigDefault(ctypes.byref(c))
         for f, _ in _CommConfig._fields_:
-            if f != "rings":
-                setattr(c, f, int(getattr(self, f)))
+            v = getattr(self, f)
+            if f != "rings" and v is not None:
+                setattr(c, f, int(v))
         keep = None
         if self.rings is not None:
             flat = [int(x) for ring in self.rings for x in ring]

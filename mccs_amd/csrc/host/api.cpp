@@ -90,7 +90,9 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   c->cfg.rings = nullptr;  // not owned
   c->nch = (int)c->rings.size();
   c->block_threads = cfg.block_threads;
-  c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, 16 / c->nch)));
+  // auto lanes: ~48 streaming workgroups per rank (one CU streams ~45 GB/s of
+  // FIFO traffic; an 8-GPU node needs ~6 links x 77 GB/s per direction)
+  c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, 48 / c->nch)));
   // every lane owns a >= 256-byte region of each 2-step slot pair (ring.hip)
   while (c->lanes > 1 && (size_t)cfg.buffer_size / MCCS_BUFFER_SLOTS * 2 / c->lanes < 256) {
     if (cfg.lanes > 0) {
@@ -156,10 +158,21 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   std::memset(cfg, 0, sizeof(*cfg));
   cfg->buffer_size = 1 << 22;
   cfg->block_threads = 512;
-  cfg->locality = MCCS_LOCALITY_SENDER;
+  // FIFO data lives with the receiver: the sender's stores cross xGMI as
+  // posted writes and every read is local HBM (the reference SHM default was
+  // Sender for host-pinned memory; both remain selectable)
+  cfg->locality = MCCS_LOCALITY_RECEIVER;
   cfg->fifo_memory = MCCS_FIFO_UNCACHED;
   cfg->work_fifo_depth = 4096;
   cfg->bridge_streams = 1;
+  // operator overrides (no rebuild needed): MCCS_LOCALITY=sender|receiver,
+  // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE
+  if (const char* v = std::getenv("MCCS_LOCALITY"))
+    cfg->locality = (v[0] == 's' || v[0] == 'S') ? MCCS_LOCALITY_SENDER : MCCS_LOCALITY_RECEIVER;
+  if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_BLOCK_THREADS")) cfg->block_threads = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_CHANNELS")) cfg->channel_count = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_BUFFER_SIZE")) cfg->buffer_size = std::atoi(v);
 }
 
 extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {

@@ -156,7 +156,8 @@ CONFIGS = [
     dict(lanes=3),
     dict(lanes=8, block_threads=256),
     dict(block_threads=1024),
-    dict(locality=C.LOCALITY_RECEIVER),
+    dict(locality=C.LOCALITY_SENDER),
+    dict(locality=C.LOCALITY_SENDER, lanes=2),
     dict(fifo_memory=C.FIFO_DEVICE),
     dict(buffer_size=1 << 20),
     dict(channel_count=2, rings="default", block_threads=544, lanes=1),  # reference profile

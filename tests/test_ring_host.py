@@ -66,7 +66,7 @@ def test_config_struct_matches_header():
     c = _CommConfig()
     lib.mccsCommConfigDefault(ctypes.byref(c))
     assert c.buffer_size == 1 << 22 and c.block_threads == 512 and c.work_fifo_depth == 4096
-    assert c.locality == comm.LOCALITY_SENDER and c.fifo_memory == comm.FIFO_UNCACHED
+    assert c.locality == comm.LOCALITY_RECEIVER and c.fifo_memory == comm.FIFO_UNCACHED
 
 
 def test_error_strings():
