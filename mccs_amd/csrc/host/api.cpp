@@ -143,8 +143,7 @@ static mccsResult_t launch_single(Comm* c, int func, int dtype, int op, const vo
   }
   if (g_group.depth == 0) {
     mccsResult_t r = plan_launch_group(g_group.comms, g_group.streams);
-    g_group.comms.clear();
-    g_group.streams.clear();
+    group_discard();
     return r;
   }
   return mccsSuccess;
@@ -180,6 +179,18 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
   std::vector<Comm*> cs(nranks, nullptr);
   mccsResult_t r = mccsSuccess;
   for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = make_comm(i, nranks, devices[i], cfg, &cs[i]);
+  // ranks sharing a GPU run as one fused launch that must be co-resident:
+  // shrink automatic lanes to fit (explicit lanes are checked at launch)
+  for (int i = 0; i < nranks && r == mccsSuccess; ++i) {
+    Comm* c = cs[i];
+    int share = 0;
+    for (int j = 0; j < nranks; ++j) share += devices[j] == devices[i];
+    if (share < 2 || c->cfg.lanes > 0) continue;
+    const int cap = coresident_ring_blocks(c->block_threads, c->device);
+    const int fit = cap / (share * c->nch);
+    if (fit < 1) r = mccsInvalidUsage;
+    else c->lanes = std::min(c->lanes, fit);
+  }
   for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_alloc_local(cs[i]);
   for (int i = 0; i < nranks && r == mccsSuccess; ++i)
     for (int j = 0; j < nranks && r == mccsSuccess; ++j) r = enable_peer(devices[i], devices[j]);
@@ -304,8 +315,7 @@ extern "C" mccsResult_t mccsGroupEnd(void) {
     return e;
   }
   mccsResult_t r = plan_launch_group(g_group.comms, g_group.streams);
-  g_group.comms.clear();
-  g_group.streams.clear();
+  group_discard();  // plans not launched after an error are dropped, not left queued
   return r;
 }
 

@@ -148,6 +148,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
 // ring.hip
 const void* ring_kernel_ptr(int func, int dtype, int op);
 const void* ring_multi_kernel_ptr(int func, int dtype, int op);
+int coresident_ring_blocks(int block, int device);
 hipError_t ring_set_device_cfg(const mccsRingKernelCfg& cfg);
 hipError_t ring_take_device_error(unsigned* err);
 hipError_t ring_flush_caches(hipStream_t st);

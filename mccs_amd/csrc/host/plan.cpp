@@ -201,6 +201,25 @@ static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
   return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
 }
 
+// Blocks of the fused multi-rank kernels the device holds at once, minimised
+// over every (func, dtype, op) instantiation.  Ranks sharing a GPU spin on
+// each other's flags, so their fused launch must be fully co-resident.
+int coresident_ring_blocks(int block, int device) {
+  DeviceGuard g(device);
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  int best = 1 << 30;
+  auto probe = [&](const void* fn) {
+    int per_cu = 0;
+    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, 0) != hipSuccess) per_cu = 0;
+    best = std::min(best, per_cu);
+  };
+  probe(ring_multi_kernel_ptr(mccsFuncAllGather, mccsInt8, 0));
+  for (int dt = 0; dt < mccsNumTypes; ++dt)
+    for (int op = 0; op < 4; ++op) probe(ring_multi_kernel_ptr(mccsFuncAllReduce, dt, op));
+  return best * ncu;
+}
+
 // Launch every pending plan.  Comms on distinct devices get one launch each
 // (on their own stream, bridged to the caller's stream with events like
 // libmccs: collectives.rs:86,134 + proxy/engine.rs:1185-1189); comms sharing a
@@ -213,6 +232,16 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
   for (auto& kv : by_dev) {
     const std::vector<int>& idx = kv.second;
     DeviceGuard g(kv.first);
+    if (idx.size() > 1) {  // checked before any work is uploaded, so the comms stay usable
+      const Comm* c0 = comms[idx[0]];
+      const int cap = coresident_ring_blocks(c0->block_threads, kv.first);
+      const long need = (long)c0->nch * c0->lanes * (long)idx.size();
+      if (need > cap) {
+        MCCS_LOG("fused launch of %zu ranks x %d blocks exceeds the %d co-resident blocks of device %d",
+                 idx.size(), c0->nch * c0->lanes, cap, kv.first);
+        return mccsInvalidUsage;  // would deadlock: every block spins on a peer's flag
+      }
+    }
     std::vector<LaunchDesc> lds(idx.size());
     for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work(comms[idx[k]], &lds[k]));
     Comm* c0 = comms[idx[0]];

@@ -218,6 +218,22 @@ def test_allgather(orc, n, nbytes):
         vnode.destroy(comms)
 
 
+def test_fused_launch_beyond_residency_fails_loudly():
+    """Explicit lanes whose fused vnode launch cannot be co-resident would
+    deadlock (every block spins on a peer's flag): refused, not hung."""
+    comms = C.init_all([0] * 8, C.CommConfig(lanes=16, block_threads=1024))
+    try:
+        import torch
+
+        x = torch.zeros(1 << 20, device="cuda")
+        with pytest.raises(C.MccsError if hasattr(C, "MccsError") else Exception):
+            with C.group():
+                for c in comms:
+                    C.all_reduce(c, x, x, 1 << 20, C.AllReduceDataType.Float32)
+    finally:
+        vnode.destroy(comms)
+
+
 def test_bad_usage_fails_loudly():
     comms = C.init_all([0, 0])
     try:
