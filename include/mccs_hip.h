@@ -17,10 +17,9 @@
 extern "C" {
 #endif
 
-/* hipStream_t / hipEvent_t are opaque pointers in the HIP C API. */
-#ifndef __HIP_PLATFORM_AMD__
+/* hipStream_t is an opaque pointer in the HIP C API; the identical typedef in
+ * hip_runtime_api.h is a compatible redeclaration (C11 / C++). */
 typedef struct ihipStream_t *hipStream_t;
-#endif
 
 /* Result codes (NCCL/mCCS convention; the reference surfaces errors as
  * Result<(), Error> in libmccs and logs CUDA errors via cuda_warning!). */
@@ -92,9 +91,9 @@ typedef struct mccsComm *mccsComm_t;
 typedef struct {
   int channel_count;    /* rings; 0 = auto: 2 x edge-disjoint Hamiltonian cycles of the node */
   int buffer_size;      /* FIFO bytes per connection (buffer_sizes[0]); 0 = 4 MiB */
-  int lanes;            /* workgroups per channel; 0 = auto */
+  int lanes;            /* workgroups per channel; 0 = auto (~48 per rank, fitted to residency) */
   int block_threads;    /* threads per workgroup (64..1024); 0 = 512 */
-  int locality;         /* MCCS_LOCALITY_*; default SENDER (reference shm default) */
+  int locality;         /* MCCS_LOCALITY_*; default RECEIVER (remote writes; SENDER = reference shm layout) */
   int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED */
   int timeout_ms;       /* FIFO spin watchdog; 0 = 30000, < 0 = never */
   int work_fifo_depth;  /* mccsDevWork slots (power of two); 0 = 4096 */

@@ -22,8 +22,8 @@ def declared_functions():
 
 def declared_kernels():
     """Reference-named kernel host stubs the header promises (symbol-level swap)."""
-    src = open(os.path.join(ROOT, "include", "mccs_hip.h")).read()
-    return set(re.findall(r"MCCS_KERNEL_SYMBOL\((\w+)\)", src))
+    src = open(os.path.join(ROOT, "include", "mccs_kernels.h")).read()
+    return set(re.findall(r"^MCCS_KERNEL_SYMBOL\((\w+)\);", src, flags=re.M))
 
 
 def exported():
@@ -51,6 +51,7 @@ def test_every_declared_symbol_has_ctypes_signature():
 
 def test_reference_kernel_symbols_exported():
     syms = exported()
+    assert len(declared_kernels()) == 41  # 4 ops x 10 types + AllGather (collectives.h:43-49)
     for k in declared_kernels():
         assert k in syms, k
 
