@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size-mib", type=int, default=128)
     ap.add_argument("--dtype", default="float32", choices=["float32", "float16", "bfloat16"])
+    ap.add_argument("--jobs", default=None, choices=["setup2"],
+                    help="N>1: two concurrent allreduce jobs on the two halves of the node (BASELINE configs[4])")
     ap.add_argument("--variant", type=int, default=0, help="reduce main loop: 0 default, 1 REG, 2 LDS")
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--policy", type=int, default=-1)
@@ -49,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of reduce variants (stderr)")
+    ap.add_argument("--sweep-reg", action="store_true", help="interleaved A/B of the REG loop's map/policy/grid")
     ap.add_argument("--no-hot", action="store_true", help="skip the same-buffer measurement (profiling)")
     return ap.parse_args()
 
@@ -162,8 +165,8 @@ def bench_reduce(args) -> dict:
             raise SystemExit("bench_reduce: result mismatch vs a+b")
         del ref
 
-    if args.sweep:
-        sweep_variants(sets, n, code, stream)
+    if args.sweep or args.sweep_reg:
+        sweep_variants(sets, n, code, stream, reg_only=args.sweep_reg)
 
     for _ in range(args.warmup):
         step()
@@ -228,7 +231,7 @@ def bench_reduce(args) -> dict:
     return out
 
 
-def sweep_variants(sets, n, code, stream):
+def sweep_variants(sets, n, code, stream, reg_only=False):
     """Interleaved rounds of reduce variants in one process, rotating buffer
     sets like the timed loop (stderr)."""
     import torch
@@ -236,17 +239,24 @@ def sweep_variants(sets, n, code, stream):
     import mccs_amd
 
     cfgs = []
-    for u in (2, 4, 8):  # REG
-        for bpc in (4, 8, 16):
-            cfgs.append((1, u, 1, bpc, 0, 0))
-    for u, s, w in ((1, 2, 4), (1, 3, 4), (1, 4, 4), (2, 2, 4), (2, 3, 4), (2, 4, 4), (4, 2, 4),
-                    (4, 3, 4), (4, 4, 4), (1, 2, 8), (1, 3, 8), (1, 4, 8), (2, 2, 8), (2, 3, 8),
-                    (2, 4, 8), (4, 2, 8)):
-        for bpc in (1, 2):
-            if w * s * 2 * u * bpc <= 160:
-                cfgs.append((2, u, 1, bpc, s, w))
-    cfgs.append((2, 2, 0, 1, 3, 4))
-    cfgs.append((1, 4, 0, 8, 0, 0))
+    if reg_only:  # REG: grid-strided (1) vs per-block contiguous (3) tiles, cache policy, grid size
+        for v in (1, 3):
+            for u in (2, 4, 8):
+                for pol in (1, 2, 3):
+                    for bpc in (8, 16, 32):
+                        cfgs.append((v, u, pol, bpc, 0, 0))
+    else:
+        for u in (2, 4, 8):  # REG
+            for bpc in (4, 8, 16):
+                cfgs.append((1, u, 1, bpc, 0, 0))
+        for u, s, w in ((1, 2, 4), (1, 3, 4), (1, 4, 4), (2, 2, 4), (2, 3, 4), (2, 4, 4), (4, 2, 4),
+                        (4, 3, 4), (4, 4, 4), (1, 2, 8), (1, 3, 8), (1, 4, 8), (2, 2, 8), (2, 3, 8),
+                        (2, 4, 8), (4, 2, 8)):  # LDS
+            for bpc in (1, 2):
+                if w * s * 2 * u * bpc <= 160:
+                    cfgs.append((2, u, 1, bpc, s, w))
+        cfgs.append((2, 2, 0, 1, 3, 4))
+        cfgs.append((1, 4, 0, 8, 0, 0))
     c0 = sets[0][2]
     alg = 3 * c0.numel() * c0.element_size()
     times = {cfg: [] for cfg in cfgs}

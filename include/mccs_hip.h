@@ -48,6 +48,7 @@ typedef enum {
 #define MCCS_REDUCE_MAX_DSTS 4
 #define MCCS_REDUCE_VARIANT_REG 1 /* register streaming main loop */
 #define MCCS_REDUCE_VARIANT_LDS 2 /* LDS-DMA multi-stage staging main loop */
+#define MCCS_REDUCE_VARIANT_REG_BLOCKED 3 /* REG with a contiguous run of tiles per block */
 
 mccsResult_t mccs_hip_reduce(void *dst, const void *const *srcs, int nsrcs, size_t count, int dtype,
                              int op, hipStream_t stream);
@@ -55,7 +56,8 @@ mccsResult_t mccs_hip_reduce_copy(void *const *dsts, int ndsts, const void *cons
                                   size_t count, int dtype, int op, hipStream_t stream);
 /* Select the main loop (0 = default), unroll = KiB per source per wave tile
  * for LDS / 16-byte packs per lane for REG (1/2/4/8, 0 = default), cache
- * policy (0 plain, 1 non-temporal, -1 default), persistent blocks per CU,
+ * policy (0 plain, 1 non-temporal, -1 default; REG only: 2 nt loads + plain
+ * stores, 3 plain loads + nt stores), persistent blocks per CU,
  * LDS ring stages (2..4) and waves per block (4/8); 0 = default for each.
  * Process-wide; for benchmarking and tests. */
 mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu, int stages,

@@ -42,7 +42,9 @@ struct ReduceArgs {
 
 // ---------------------------------------------------------------------------
 // REG: NS/ND > 0 are compile-time source/destination counts; 0 = runtime.
-template <int DT, int OP, int NS, int ND, int U, int LDP, int STP>
+// MAP 0: tiles grid-strided over blocks (the chip sweeps one contiguous window);
+// MAP 1: each block owns a contiguous run of tiles (2048+ independent streams).
+template <int DT, int OP, int NS, int ND, int U, int LDP, int STP, int MAP = 0>
 __global__ void __launch_bounds__(256) reduce_reg_kernel(ReduceArgs a) {
   using T = typename Elem<DT>::T;
   constexpr int PACK = kPackElems<DT>;
@@ -55,7 +57,12 @@ __global__ void __launch_bounds__(256) reduce_reg_kernel(ReduceArgs a) {
   const int64_t tile = (int64_t)B * U;
   const int tid = threadIdx.x;
 
-  for (int64_t t = blockIdx.x; t * tile < npack; t += gridDim.x) {
+  const int64_t ntiles = (npack + tile - 1) / tile;
+  const int64_t per = MAP ? (ntiles + gridDim.x - 1) / gridDim.x : 0;
+  const int64_t t0 = MAP ? (int64_t)blockIdx.x * per : blockIdx.x;
+  const int64_t t1 = MAP ? (t0 + per < ntiles ? t0 + per : ntiles) : ntiles;
+  const int64_t tstep = MAP ? 1 : gridDim.x;
+  for (int64_t t = t0; t < t1; t += tstep) {
     const int64_t base = t * tile + tid;
     if ((t + 1) * tile <= npack) {
       u32x4 v[U];
@@ -256,24 +263,43 @@ static int num_cus() {
   return n;
 }
 
-template <int DT, int OP, int NS, int ND, int U>
+template <int DT, int OP>
+constexpr bool tuned_grid() { return OP == OpSum && (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16); }
+
+// pol: 0 plain, 1 nt loads + nt stores, 2 nt loads + plain stores,
+// 3 plain loads + nt stores (2/3 and map 1 only in the tuning grid).
+template <int DT, int OP, int NS, int ND, int U, int MAP>
 static hipError_t launch_reg(const ReduceArgs& a, int pol, int grid, hipStream_t st) {
-  if (pol)
-    hipLaunchKernelGGL((reduce_reg_kernel<DT, OP, NS, ND, U, kNonTemporal, kNonTemporal>), dim3(grid),
-                       dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((reduce_reg_kernel<DT, OP, NS, ND, U, kPlain, kPlain>), dim3(grid), dim3(256),
-                       0, st, a);
+#define MCCS_REG(LP, SP) \
+  hipLaunchKernelGGL((reduce_reg_kernel<DT, OP, NS, ND, U, LP, SP, MAP>), dim3(grid), dim3(256), 0, st, a)
+  if constexpr (tuned_grid<DT, OP>()) {
+    if (pol == 2) {
+      MCCS_REG(kNonTemporal, kPlain);
+      return hipGetLastError();
+    }
+    if (pol == 3) {
+      MCCS_REG(kPlain, kNonTemporal);
+      return hipGetLastError();
+    }
+  }
+  if (pol) MCCS_REG(kNonTemporal, kNonTemporal);
+  else MCCS_REG(kPlain, kPlain);
+#undef MCCS_REG
   return hipGetLastError();
 }
 
 template <int DT, int OP, int NS, int ND>
-static hipError_t launch_reg_u(const ReduceArgs& a, int u, int pol, int grid, hipStream_t st) {
-  if constexpr (OP == OpSum && (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16)) {
-    if (u == 2) return launch_reg<DT, OP, NS, ND, 2>(a, pol, grid, st);
-    if (u == 8) return launch_reg<DT, OP, NS, ND, 8>(a, pol, grid, st);
+static hipError_t launch_reg_u(const ReduceArgs& a, int u, int pol, int map, int grid, hipStream_t st) {
+  if constexpr (tuned_grid<DT, OP>()) {
+    if (map) {
+      if (u == 2) return launch_reg<DT, OP, NS, ND, 2, 1>(a, pol, grid, st);
+      if (u == 8) return launch_reg<DT, OP, NS, ND, 8, 1>(a, pol, grid, st);
+      return launch_reg<DT, OP, NS, ND, 4, 1>(a, pol, grid, st);
+    }
+    if (u == 2) return launch_reg<DT, OP, NS, ND, 2, 0>(a, pol, grid, st);
+    if (u == 8) return launch_reg<DT, OP, NS, ND, 8, 0>(a, pol, grid, st);
   }
-  return launch_reg<DT, OP, NS, ND, 4>(a, pol, grid, st);
+  return launch_reg<DT, OP, NS, ND, 4, 0>(a, pol, grid, st);
 }
 
 template <int U, int S, int W>
@@ -343,17 +369,19 @@ static hipError_t dispatch(const ReduceArgs& a, hipStream_t st) {
     if (ok) return e;
     // untuned (U,S,W) for this dtype/op: fall through to the REG loop
   }
-  const int unroll = t.variant == MCCS_REDUCE_VARIANT_REG ? t.unroll : 4;
-  const int bpc = t.variant == MCCS_REDUCE_VARIANT_REG ? t.blocks_per_cu : 16;
+  const bool reg = t.variant == MCCS_REDUCE_VARIANT_REG || t.variant == MCCS_REDUCE_VARIANT_REG_BLOCKED;
+  const int map = t.variant == MCCS_REDUCE_VARIANT_REG_BLOCKED ? 1 : 0;
+  const int unroll = reg ? t.unroll : 4;
+  const int bpc = reg ? t.blocks_per_cu : 16;
   const int64_t npack = a.count / PACK;
   const int64_t tile = 256LL * unroll;
   int64_t tiles = (npack + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
   const int64_t gmax = (int64_t)cus * (bpc > 0 ? bpc : 8);
   const int grid = (int)(tiles < gmax ? tiles : gmax);
-  if (a.nsrcs == 2 && a.ndsts == 1) return launch_reg_u<DT, OP, 2, 1>(a, unroll, t.policy, grid, st);
-  if (a.nsrcs == 1 && a.ndsts == 1) return launch_reg_u<DT, OP, 1, 1>(a, unroll, t.policy, grid, st);
-  return launch_reg<DT, OP, 0, 0, 4>(a, t.policy, grid, st);
+  if (a.nsrcs == 2 && a.ndsts == 1) return launch_reg_u<DT, OP, 2, 1>(a, unroll, t.policy, map, grid, st);
+  if (a.nsrcs == 1 && a.ndsts == 1) return launch_reg_u<DT, OP, 1, 1>(a, unroll, t.policy, 0, grid, st);
+  return launch_reg<DT, OP, 0, 0, 4, 0>(a, t.policy ? 1 : 0, grid, st);
 }
 
 template <int DT>
@@ -412,16 +440,17 @@ extern "C" mccsResult_t mccs_hip_reduce(void* dst, const void* const* srcs, int 
 
 extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu,
                                              int stages, int waves) {
-  if (variant < 0 || variant > MCCS_REDUCE_VARIANT_LDS) return mccsInvalidArgument;
+  if (variant < 0 || variant > MCCS_REDUCE_VARIANT_REG_BLOCKED) return mccsInvalidArgument;
+  if (policy > 3) return mccsInvalidArgument;
   if (unroll < 0 || unroll > 8 || (unroll & (unroll - 1))) return mccsInvalidArgument;
   if (stages < 0 || stages == 1 || stages > 4 || waves < 0 || (waves != 0 && waves != 4 && waves != 8))
     return mccsInvalidArgument;
   ReduceTune d;
   ReduceTune t;
   t.variant = variant ? variant : d.variant;
-  const bool reg = t.variant == MCCS_REDUCE_VARIANT_REG;
+  const bool reg = t.variant != MCCS_REDUCE_VARIANT_LDS;
   t.unroll = unroll ? unroll : (reg ? 4 : 2);
-  t.policy = policy < 0 ? d.policy : (policy ? 1 : 0);
+  t.policy = policy < 0 ? d.policy : (reg ? policy : (policy ? 1 : 0));
   t.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : (reg ? 16 : 1);
   t.stages = stages ? stages : d.stages;
   t.waves = waves ? waves : d.waves;

@@ -32,12 +32,12 @@ def _exchange_factory(dist, world):
     return exchange
 
 
-def agree(dist, ok: bool) -> bool:
+def agree(dist, ok: bool, group=None) -> bool:
     """True only if every rank passed (MIN over ranks)."""
     import torch
 
     t = torch.tensor([1 if ok else 0], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return bool(t.item() == 1)
 
 
@@ -64,6 +64,122 @@ def _expected_exact(torch, n_elem, world, dev):
     return tot.to(torch.float64).div(64.0).to(torch.float32)
 
 
+WORKLOADS = {
+    ("float32", 128): "BASELINE configs[2]",
+    ("float16", 1024): "BASELINE configs[3]",
+}
+
+# BASELINE configs[4]: workloads/setup-2_vgg.toml (fp16, 574,668,960 B) and
+# setup-2_gpt_1.toml (fp16, 83,886,080 B), one job per half of the node.
+SETUP2_JOBS = (("setup-2_vgg", 287_334_480), ("setup-2_gpt_1", 41_943_040))
+
+# name -> (bench dtype tag, AllReduceDataType member, kernel symbol suffix)
+DTYPES = {"float32": ("f32", "Float32", "float"), "float16": ("f16", "Float16", "half"),
+          "bfloat16": ("bf16", "Bfloat16", "bfloat16")}
+
+
+def _subgroup_exchange(dist, group, n):
+    def exchange(b: bytes):
+        out = [None] * n
+        dist.all_gather_object(out, b, group=group)
+        return out
+
+    return exchange
+
+
+def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, group=None):
+    """Build the communicator; check an exact-sum fp32 AllReduce bit for bit
+    on every rank; on failure rebuild with cached FIFOs + system fences."""
+    attempts = [("uncached-fifo", C.CommConfig(timeout_ms=60000)),
+                ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000))]
+    for name, cfg in attempts:
+        comm = C.init_communicator_rank(rank, world, device, exchange, cfg)
+        nv = (4 << 20) // 4  # 4 MiB exact-sum fp32 check (multi-loop, ragged chunks)
+        xv = _exact_inputs(torch, nv, rank, dev)
+        yv = torch.empty_like(xv)
+        ok = True
+        try:
+            C.all_reduce(comm, xv, yv, nv, C.AllReduceDataType.Float32)
+            comm.sync()
+            torch.cuda.synchronize()
+            ok = bool(torch.equal(yv, _expected_exact(torch, nv, world, dev)))
+        except Exception as e:  # noqa: BLE001  (watchdog / HIP error: try the next mode)
+            print(f"[rank {rank}] {name}: {e}", flush=True)
+            ok = False
+        if agree(dist, ok, group):
+            return comm, name
+        comm.destroy()
+    raise SystemExit("ring allreduce failed validation in every FIFO mode")
+
+
+def _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev) -> bool:
+    """BASELINE-size check through a size-independent property: k/64 inputs
+    (|k| <= 255) sum exactly in fp16/bf16/fp32 for <= 8 ranks, so the
+    AllReduce must equal the integer sum bit for bit in any order."""
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    k = ((i * 7 + rank * 13) % 511) - 255
+    x = (k.to(torch.float32) / 64.0).to(tdt)
+    del k
+    y = torch.empty_like(x)
+    C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum)
+    comm.sync()
+    tot = torch.zeros(n, device=dev, dtype=torch.int64)
+    for r in range(world):
+        tot += ((i * 7 + r * 13) % 511) - 255
+    exp = (tot.to(torch.float64) / 64.0).to(tdt)
+    ok = bool(torch.equal(y, exp)) if world <= 8 else True
+    del x, y, tot, exp, i
+    torch.cuda.empty_cache()
+    return ok
+
+
+def _out_links(rings, rank):
+    """Distinct xGMI links this rank sends on (one per distinct ring successor)."""
+    nxt = set()
+    for order in rings:
+        p = order.index(rank)
+        nxt.add(order[(p + 1) % len(order)])
+    return len(nxt)
+
+
+def _time_steps(torch, dist, comm, step, warmup, K, group=None):
+    for _ in range(warmup):
+        step()
+    comm.sync()
+    torch.cuda.synchronize()
+    dist.barrier(group=group)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize()
+    comm.sync()
+    t1 = time.perf_counter()
+    dist.barrier(group=group)
+    return t1 - t0
+
+
+def cpu_ring_baseline(C, world: int, budget_s: float = 3.0) -> dict:
+    """The same ring schedule on host threads (mccs_host_ring_allreduce, the
+    configs[0] plumbing) over a bounded fp32 sample, for scale."""
+    import numpy as np
+
+    n = (16 << 20) // 4
+    rng = np.random.default_rng(0)
+    send = [(rng.random(n, dtype=np.float32) * 2 - 1) for _ in range(world)]
+    recv = [np.empty_like(x) for x in send]
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        C.host_ring_allreduce(send, recv, n, C.AllReduceDataType.Float32, channels=2, nthreads=544)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(n * 4 / dt / 1e9, 3), "unit": "GB/s algbw", "cores": 2 * world, "kind": "port",
+            "sample": f"{world} ranks x 16 MiB fp32, host-thread ring (2 channels), {reps} reps"}
+
+
 def run(args):
     import torch
     import torch.distributed as dist
@@ -79,42 +195,18 @@ def run(args):
     dev = torch.device("cuda", device)
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if getattr(args, "jobs", None) == "setup2":
+        return run_setup2(args, torch, dist, C, rank, world, device, dev)
     exchange = _exchange_factory(dist, world)
 
     dt_name = args.dtype
     tdt = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[dt_name]
-    code = {"float32": C.AllReduceDataType.Float32, "float16": C.AllReduceDataType.Float16,
-            "bfloat16": C.AllReduceDataType.Bfloat16}[dt_name]
+    code = getattr(C.AllReduceDataType, DTYPES[dt_name][1])
     esize = torch.tensor([], dtype=tdt).element_size()
     nbytes = args.size_mib << 20
     n = nbytes // esize
 
-    attempts = [("uncached-fifo", C.CommConfig(timeout_ms=60000)),
-                ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000))]
-    comm = None
-    mode = None
-    validated = False
-    for name, cfg in attempts:
-        comm = C.init_communicator_rank(rank, world, device, exchange, cfg)
-        nv = (4 << 20) // 4  # 4 MiB exact-sum fp32 check (multi-loop, ragged chunks)
-        xv = _exact_inputs(torch, nv, rank, dev)
-        yv = torch.empty_like(xv)
-        ok = True
-        try:
-            C.all_reduce(comm, xv, yv, nv, C.AllReduceDataType.Float32)
-            comm.sync()
-            torch.cuda.synchronize()
-            ok = bool(torch.equal(yv, _expected_exact(torch, nv, world, dev)))
-        except Exception as e:  # noqa: BLE001  (watchdog / HIP error: try the next mode)
-            print(f"[rank {rank}] {name}: {e}", flush=True)
-            ok = False
-        if agree(dist, ok):
-            mode, validated = name, True
-            break
-        comm.destroy()
-        comm = None
-    if comm is None:
-        raise SystemExit("ring allreduce failed validation in every FIFO mode")
+    comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange)
 
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
@@ -125,34 +217,20 @@ def run(args):
     def step():
         C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, stream)
 
-    for _ in range(args.warmup):
-        step()
-    comm.sync()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
     K = args.steps
-    for _ in range(K):
-        step()
-    torch.cuda.synchronize()
-    comm.sync()
-    t1 = time.perf_counter()
-    dist.barrier()
-    elapsed = max_over_ranks(dist, t1 - t0)
+    elapsed = max_over_ranks(dist, _time_steps(torch, dist, comm, step, args.warmup, K))
     per_step = elapsed / K
+    del x, y
+    full_ok = agree(dist, _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev))
     algbw = nbytes / per_step / 1e9
     busbw = algbw * 2 * (world - 1) / world
-    # per-rank HBM bytes the ring moves (local reads/writes of user buffers and
-    # FIFO slots): send input S/n, (n-2) x [read input + FIFO, write FIFO],
-    # final [read input + FIFO, write output + FIFO], (n-2) x [read FIFO,
-    # write output + FIFO], last [read FIFO, write output]
-    s = nbytes
-    hbm_bytes = s / world * (1 + 1 + (world - 2) * 3 + 4 + (world - 2) * 3 + 2)
-    link_bytes = 2 * (world - 1) / world * s
+    link_bytes = 2 * (world - 1) / world * nbytes
     out = None
     if rank == 0:
-        nch = comm.nchannels
+        rings = comm.rings()
+        links = _out_links(rings, 0)
+        link_gbps = link_bytes / per_step / 1e9
+        peak = links * XGMI_LINK_GBPS_PER_DIR
         out = {
             "metric": "device-resident reduce GB/s; ring-allreduce algbw GB/s at 1/2/4/8 MI355X",
             "submetric": "ring_allreduce_algbw_GBps",
@@ -165,35 +243,94 @@ def run(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"float32": "f32", "float16": "f16", "bfloat16": "bf16"}[dt_name],
+            "dtype": DTYPES[dt_name][0],
             "data": "synthetic uniform[-1,1) per rank, device-resident buckets",
             "config": {
                 "workload": f"{world}x MI355X ring allreduce over xGMI P2P, {args.size_mib} MiB {dt_name} "
-                            f"buckets, chunked FIFO pipeline (BASELINE configs[2])",
-                "bytes_per_rank": nbytes, "channels": nch, "lanes": comm.lanes,
-                "block_threads": comm.block_threads, "rings": comm.rings(), "fifo_mode": mode,
-                "validated_exact_sum": validated, "busbw_GBps": round(busbw, 3),
-                "parallelism": f"ring{world}",
+                            f"buckets, chunked FIFO pipeline ({WORKLOADS.get((dt_name, args.size_mib), 'custom')})",
+                "bytes_per_rank": nbytes, "channels": comm.nchannels, "lanes": comm.lanes,
+                "block_threads": comm.block_threads, "rings": rings, "fifo_mode": mode,
+                "validated_exact_sum_4MiB": True, "validated_exact_sum_full_size": full_ok,
+                "busbw_GBps": round(busbw, 3), "parallelism": f"ring{world}",
+                # ranks sharing one GPU (a 1-GPU box): FIFO hand-offs stay in HBM, no xGMI link
+                "ranks_share_gpu": ndev < world,
             },
+            # the ring's bound is the xGMI links it sends on, not HBM
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(hbm_bytes / per_step / 1e9, 2),
-                "peak": 8000.0,
+                "bound": "xgmi",
+                "achieved": round(link_gbps, 2),
+                "peak": peak,
                 "unit": "GB/s",
-                "frac": round(hbm_bytes / per_step / 1e9 / 8000.0, 5),
+                "frac": round(link_gbps / peak, 4),
                 "traffic": None,
-                "kernel": "mccsKernel_AllReduce_RING_SIMPLE_Sum",
-                "note": "ring is xGMI-link bound; see xgmi",
-            },
-            "xgmi": {
-                "link_bytes_per_rank": int(link_bytes),
-                "achieved_GBps_per_rank": round(link_bytes / per_step / 1e9, 2),
-                "rings_per_rank_out_links": nch,
-                "assumed_link_GBps_per_direction": XGMI_LINK_GBPS_PER_DIR,
+                "kernel": "mccsKernel_AllReduce_RING_SIMPLE_Sum_" + DTYPES[dt_name][2],
+                "note": f"per-rank link bytes 2(n-1)/n*S over {links} distinct outgoing links x "
+                        f"{XGMI_LINK_GBPS_PER_DIR} GB/s per direction (spec)",
             },
             "cpu_baseline": None,
         }
+        if not getattr(args, "no_cpu_baseline", False):
+            out["cpu_ring_baseline"] = cpu_ring_baseline(C, world)
     comm.destroy()
     dist.barrier()
     dist.destroy_process_group()
+    if not full_ok:
+        raise SystemExit("full-size exact-sum AllReduce mismatch")
     return out
+
+
+def run_setup2(args, torch, dist, C, rank, world, device, dev):
+    """BASELINE configs[4]: two concurrent AllReduce jobs, one per half of the
+    node (disjoint GPU sets), shapes from workloads/setup-2_{vgg,gpt_1}.toml.
+    Each job times its own K calls; both run at the same time."""
+    if world < 4 or world % 2:
+        raise SystemExit("--jobs setup2 needs an even world size >= 4")
+    half = world // 2
+    groups = [dist.new_group(list(range(0, half))), dist.new_group(list(range(half, world)))]
+    job = 0 if rank < half else 1
+    jrank = rank - job * half
+    grp = groups[job]
+    exchange = _subgroup_exchange(dist, grp, half)
+    comm, mode = _make_validated_comm(torch, dist, C, jrank, half, device, dev, exchange, grp)
+    name, n = SETUP2_JOBS[job]
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000 + rank)
+    x = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(torch.float16)
+    y = torch.empty_like(x)
+
+    def step():
+        C.all_reduce(comm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum)
+
+    dist.barrier()  # both jobs start together
+    el = _time_steps(torch, dist, comm, step, args.warmup, args.steps, grp)
+    t = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
+    per_job = torch.zeros(2, dtype=torch.float64)
+    per_job[job] = t[0] / args.steps
+    dist.all_reduce(per_job, op=dist.ReduceOp.MAX)
+    comm.destroy()
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank != 0:
+        return None
+    jobs = []
+    for j, (nm, cnt) in enumerate(SETUP2_JOBS):
+        ps = float(per_job[j])
+        jobs.append({"job": nm, "ranks": half, "bytes": cnt * 2, "ms_per_call": round(ps * 1e3, 4),
+                     "algbw_GBps": round(cnt * 2 / ps / 1e9, 3)})
+    return {
+        "metric": "device-resident reduce GB/s; ring-allreduce algbw GB/s at 1/2/4/8 MI355X",
+        "submetric": "concurrent_jobs_algbw_GBps",
+        "value": round(sum(j["algbw_GBps"] for j in jobs), 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": "synthetic uniform[-1,1) per rank, device-resident buckets",
+        "config": {"workload": "2 concurrent allreduce jobs on disjoint GPU halves, setup-2 shapes "
+                               "(BASELINE configs[4])", "jobs": jobs, "fifo_mode": mode},
+    }

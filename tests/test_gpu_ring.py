@@ -248,3 +248,38 @@ def test_bad_usage_fails_loudly():
                 C.all_reduce(comms[0], x, x, 16, C.AllReduceDataType.Float16)  # mixed plan
     finally:
         vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("code,mib", [(F32, 128), (F16, 1024)], ids=["configs2-fp32-128MiB", "configs3-fp16-1GiB"])
+def test_baseline_sizes_exact(code, mib):
+    """BASELINE configs[2]/[3] bucket sizes on an 8-rank virtual node through a
+    size-independent property: k/64 inputs (|k| <= 255) sum exactly in fp16 and
+    fp32 for 8 ranks, so every rank must hold the integer sum / 64 bit for bit
+    (the order-independent golden vectors of nccl-tests verifiable.cu:419-520)."""
+    import torch
+
+    n = 8
+    tdt = {F32: torch.float32, F16: torch.float16}[code]
+    count = (mib << 20) // (4 if code == F32 else 2)
+    comms = C.init_all([0] * n)
+    try:
+        i = torch.arange(count, device="cuda", dtype=torch.int64)
+        tot = torch.zeros(count, device="cuda", dtype=torch.int64)
+        send = []
+        for r in range(n):
+            k = ((i * 7 + r * 13) % 511) - 255
+            tot += k
+            send.append((k.to(torch.float32) / 64.0).to(tdt))
+            del k
+        exp = (tot.to(torch.float64) / 64.0).to(tdt)
+        del tot, i
+        recv = [torch.empty_like(x) for x in send]
+        with C.group():
+            for r in range(n):
+                C.all_reduce(comms[r], send[r], recv[r], count, code, 0)
+        for c in comms:
+            c.sync()
+        for r in range(n):
+            assert torch.equal(recv[r], exp), f"rank {r}"
+    finally:
+        vnode.destroy(comms)
