@@ -47,7 +47,7 @@ static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
   // granule (512 x 8 B, all_reduce.h:34-35) so a rounded chunk fits 4 steps
   if (c.buffer_size < 8192 || c.buffer_size % 8192 != 0) return mccsInvalidArgument;
   // multiples of 32 keep the reference's nWarps*32 blocks (e.g. 544) valid
-  if (c.block_threads < 64 || c.block_threads > 1024 || c.block_threads % 32) return mccsInvalidArgument;
+  if (c.block_threads < 64 || c.block_threads > MCCS_RING_MAX_THREADS || c.block_threads % 32) return mccsInvalidArgument;
   if (c.lanes < 0 || c.lanes > MCCS_MAX_LANES) return mccsInvalidArgument;
   if (c.channel_count < 0 || c.channel_count > MCCS_MAX_NCHANNELS) return mccsInvalidArgument;
   if (c.work_fifo_depth & (c.work_fifo_depth - 1)) return mccsInvalidArgument;
@@ -90,9 +90,11 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   c->cfg.rings = nullptr;  // not owned
   c->nch = (int)c->rings.size();
   c->block_threads = cfg.block_threads;
-  // auto lanes: ~48 streaming workgroups per rank (one CU streams ~45 GB/s of
-  // FIFO traffic; an 8-GPU node needs ~6 links x 77 GB/s per direction)
-  c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, 48 / c->nch)));
+  // auto lanes: ~64 streaming workgroups per rank.  A lane's throughput is
+  // bound by its per-slice latency chain (flag poll, loads, store drain), not
+  // by bandwidth, and the virtual-node sweep scales ~linearly in lanes up to
+  // 16 per channel; an 8-GPU rank must feed 6 links x ~77 GB/s per direction.
+  c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, 64 / c->nch)));
   // every lane owns a >= 256-byte region of each 2-step slot pair (ring.hip)
   while (c->lanes > 1 && (size_t)cfg.buffer_size / MCCS_BUFFER_SLOTS * 2 / c->lanes < 256) {
     if (cfg.lanes > 0) {

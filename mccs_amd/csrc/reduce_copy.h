@@ -76,17 +76,41 @@ __device__ __forceinline__ void reduce_copy_group(const void* const* srcs, int n
         }
       }
     }
-    // remainder packs, one at a time
-    for (; p < npack; p += nthr) {
-      u32x4 v = ld16<(NTMASK & 1) ? kNonTemporal : LDPOL>((const u32x4*)srcs[0] + p);
+    // remainder (< U packs per thread): one predicated U-deep pass, so every
+    // load is in flight at once instead of one memory round trip per pack
+    if (p < npack) {
+      u32x4 v[U];
 #pragma unroll
-      for (int s = 1; s < MAXS; ++s)
-        if (s < nsrcs)
-          v = pack_op<DT, OP>(v, ((NTMASK >> s) & 1) ? ld16<kNonTemporal>((const u32x4*)srcs[s] + p)
-                                                     : ld16<LDPOL>((const u32x4*)srcs[s] + p));
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = p + (int64_t)u * nthr;
+        if (q < npack) v[u] = ld16<(NTMASK & 1) ? kNonTemporal : LDPOL>((const u32x4*)srcs[0] + q);
+      }
 #pragma unroll
-      for (int d = 0; d < MAXD; ++d)
-        if (d < ndsts) st16<STPOL>((u32x4*)dsts[d] + p, v);
+      for (int s = 1; s < MAXS; ++s) {
+        if (s < nsrcs) {
+          u32x4 w[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int64_t q = p + (int64_t)u * nthr;
+            if (q < npack)
+              w[u] = ((NTMASK >> s) & 1) ? ld16<kNonTemporal>((const u32x4*)srcs[s] + q)
+                                         : ld16<LDPOL>((const u32x4*)srcs[s] + q);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (p + (int64_t)u * nthr < npack) v[u] = pack_op<DT, OP>(v[u], w[u]);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < MAXD; ++d) {
+        if (d < ndsts) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int64_t q = p + (int64_t)u * nthr;
+            if (q < npack) st16<STPOL>((u32x4*)dsts[d] + q, v[u]);
+          }
+        }
+      }
     }
     done = npack * PACK;
   }
@@ -101,6 +125,91 @@ __device__ __forceinline__ void reduce_copy_group(const void* const* srcs, int n
 #pragma unroll
     for (int d = 0; d < MAXD; ++d)
       if (d < ndsts) ((T*)dsts[d])[e] = v;
+  }
+}
+
+
+// Ring-step reduce-copy with the operand shape fixed at compile time (the
+// ring primitive knows it: NS sources, ND destinations) and a wave-contiguous
+// layout: wave w of the group owns U consecutive 1 KiB rows of each U*W KiB
+// iteration, lane l reads 16 bytes at row offset 16*l, so every load/store
+// instruction moves 1 KiB contiguous and the U rows of a wave sit at constant
+// 1 KiB strides from one 32-bit per-lane offset (uniform 64-bit bases stay in
+// SGPRs; no per-pack 64-bit address registers).  All U x NS loads of an
+// iteration are issued before the first use; the partial last iteration is a
+// single predicated pass.  Every pointer must be 16-byte aligned when
+// ALIGNED; otherwise a typed element loop runs (reference ReduceCopyMulti).
+template <int DT, int OP, int U, int NS, int ND, int NTMASK>
+__device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1, void* d0, void* d1, int64_t nelem,
+                                                 int tid, int nthr) {
+  static_assert(NS >= 1 && NS <= 2 && ND >= 1 && ND <= 2, "ring primitives move 1-2 sources to 1-2 destinations");
+  using T = typename Elem<DT>::T;
+  constexpr int PACK = kPackElems<DT>;
+  if (nelem <= 0) return;
+  uintptr_t mis = (uintptr_t)s0 | (uintptr_t)d0;
+  if constexpr (NS > 1) mis |= (uintptr_t)s1;
+  if constexpr (ND > 1) mis |= (uintptr_t)d1;
+  int64_t done = 0;
+  if ((mis & 15) == 0) {
+    const u32x4* a = (const u32x4*)s0;
+    const u32x4* b = (const u32x4*)s1;
+    u32x4* x = (u32x4*)d0;
+    u32x4* y = (u32x4*)d1;
+    const uint32_t npack = (uint32_t)(nelem / PACK);
+    const uint32_t wave = (uint32_t)tid >> 6, lane = (uint32_t)tid & 63;
+    const uint32_t per_iter = (uint32_t)nthr * U;  // packs
+    const uint32_t mine = wave * (64u * U) + lane;   // first pack of this lane in an iteration
+    uint32_t base = 0;
+    for (; base + per_iter <= npack; base += per_iter) {
+      const uint32_t q = base + mine;
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16<(NTMASK & 1) ? kNonTemporal : kPlain>(a + q + 64u * u);
+      if constexpr (NS > 1) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = ld16<(NTMASK & 2) ? kNonTemporal : kPlain>(b + q + 64u * u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = pack_op<DT, OP>(v[u], w[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) st16<kPlain>(x + q + 64u * u, v[u]);
+      if constexpr (ND > 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) st16<kPlain>(y + q + 64u * u, v[u]);
+      }
+    }
+    if (base < npack) {  // partial iteration: same layout, predicated
+      const uint32_t q = base + mine;
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (q + 64u * u < npack) v[u] = ld16<(NTMASK & 1) ? kNonTemporal : kPlain>(a + q + 64u * u);
+      if constexpr (NS > 1) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (q + 64u * u < npack) w[u] = ld16<(NTMASK & 2) ? kNonTemporal : kPlain>(b + q + 64u * u);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (q + 64u * u < npack) v[u] = pack_op<DT, OP>(v[u], w[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (q + 64u * u < npack) {
+          st16<kPlain>(x + q + 64u * u, v[u]);
+          if constexpr (ND > 1) st16<kPlain>(y + q + 64u * u, v[u]);
+        }
+    }
+    done = (int64_t)npack * PACK;
+  }
+  // typed scalar tail / unaligned fallback
+  for (int64_t e = done + tid; e < nelem; e += nthr) {
+    T v = (NTMASK & 1) ? __builtin_nontemporal_load((const T*)s0 + e) : ((const T*)s0)[e];
+    if constexpr (NS > 1)
+      v = scalar_op<DT, OP>(v, (NTMASK & 2) ? __builtin_nontemporal_load((const T*)s1 + e) : ((const T*)s1)[e]);
+    ((T*)d0)[e] = v;
+    if constexpr (ND > 1) ((T*)d1)[e] = v;
   }
 }
 

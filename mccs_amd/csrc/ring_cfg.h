@@ -14,6 +14,11 @@
 #define MCCS_FLAG_LINE_BYTES 128
 #define MCCS_FLAG_LINE_WORDS (MCCS_FLAG_LINE_BYTES / 8)
 #define MCCS_MAX_LANES 16
+// Largest ring workgroup.  576 = 9 waves covers the reference's 17-warp (544
+// thread) blocks (get_task_schema, plan.rs:602-635) and keeps ~168 VGPRs per
+// lane (3 waves per SIMD): the fully inlined ring loop with 8 packs in flight
+// per source fits without spilling, which a 1024-thread bound (128 VGPRs) did not.
+#define MCCS_RING_MAX_THREADS 576
 
 // Fence policy for FIFO hand-offs (device global, per device; set by the host).
 #define MCCS_FENCE_SYSTEM 0   // FIFO memory may be cached: system-scope release/acquire

@@ -155,7 +155,7 @@ CONFIGS = [
     dict(lanes=1),
     dict(lanes=3),
     dict(lanes=8, block_threads=256),
-    dict(block_threads=1024),
+    dict(block_threads=576),
     dict(locality=C.LOCALITY_SENDER),
     dict(locality=C.LOCALITY_SENDER, lanes=2),
     dict(fifo_memory=C.FIFO_DEVICE),
@@ -221,7 +221,7 @@ def test_allgather(orc, n, nbytes):
 def test_fused_launch_beyond_residency_fails_loudly():
     """Explicit lanes whose fused vnode launch cannot be co-resident would
     deadlock (every block spins on a peer's flag): refused, not hung."""
-    comms = C.init_all([0] * 8, C.CommConfig(lanes=16, block_threads=1024))
+    comms = C.init_all([0] * 8, C.CommConfig(lanes=16, block_threads=576))
     try:
         import torch
 
