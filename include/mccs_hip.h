@@ -99,7 +99,7 @@ typedef struct {
   int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED */
   int timeout_ms;       /* FIFO spin watchdog; 0 = 30000, < 0 = never */
   int work_fifo_depth;  /* mccsDevWork slots (power of two); 0 = 4096 */
-  int bridge_streams;   /* 1 (default): user stream -> comm stream events (libmccs semantics); -1: launch on user stream */
+  int bridge_streams;   /* -1 (default): launch on the caller's stream; 1: user stream -> comm stream -> user stream events (libmccs two-stream bridge) */
   const int *rings;     /* channel_count x nranks send orders (comm_patterns_override); NULL = auto */
 } mccsCommConfig;
 

@@ -39,7 +39,10 @@ static void fill_defaults(mccsCommConfig* c) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
   if (c->block_threads <= 0) c->block_threads = 512;
   if (c->work_fifo_depth <= 0) c->work_fifo_depth = 4096;
-  if (c->bridge_streams == 0) c->bridge_streams = 1;
+  // launch on the caller's stream (stream order is the same as libmccs's
+  // user-event -> comm-stream -> backend-event bridge, without the ~10 us per
+  // cross-stream wait measured on MI355X); 1 keeps the two-stream bridge
+  if (c->bridge_streams == 0) c->bridge_streams = -1;
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
@@ -165,12 +168,13 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   cfg->locality = MCCS_LOCALITY_RECEIVER;
   cfg->fifo_memory = MCCS_FIFO_UNCACHED;
   cfg->work_fifo_depth = 4096;
-  cfg->bridge_streams = 1;
+  cfg->bridge_streams = -1;
   // operator overrides (no rebuild needed): MCCS_LOCALITY=sender|receiver,
   // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE
   if (const char* v = std::getenv("MCCS_LOCALITY"))
     cfg->locality = (v[0] == 's' || v[0] == 'S') ? MCCS_LOCALITY_SENDER : MCCS_LOCALITY_RECEIVER;
   if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_BRIDGE_STREAMS")) cfg->bridge_streams = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BLOCK_THREADS")) cfg->block_threads = std::atoi(v);
   if (const char* v = std::getenv("MCCS_CHANNELS")) cfg->channel_count = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BUFFER_SIZE")) cfg->buffer_size = std::atoi(v);

@@ -20,6 +20,7 @@
 #include <atomic>
 #include <cstring>
 #include <map>
+#include <mutex>
 
 #include "comm.h"
 #include "dtypes.h"
@@ -205,6 +206,13 @@ static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
 // over every (func, dtype, op) instantiation.  Ranks sharing a GPU spin on
 // each other's flags, so their fused launch must be fully co-resident.
 int coresident_ring_blocks(int block, int device) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;  // (device, block) -> blocks
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({device, block});
+    if (it != cache.end()) return it->second;
+  }
   DeviceGuard g(device);
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
@@ -217,14 +225,17 @@ int coresident_ring_blocks(int block, int device) {
   probe(ring_multi_kernel_ptr(mccsFuncAllGather, mccsInt8, 0));
   for (int dt = 0; dt < mccsNumTypes; ++dt)
     for (int op = 0; op < 4; ++op) probe(ring_multi_kernel_ptr(mccsFuncAllReduce, dt, op));
-  return best * ncu;
+  std::lock_guard<std::mutex> lk(mu);
+  return cache[{device, block}] = best * ncu;
 }
 
-// Launch every pending plan.  Comms on distinct devices get one launch each
-// (on their own stream, bridged to the caller's stream with events like
-// libmccs: collectives.rs:86,134 + proxy/engine.rs:1185-1189); comms sharing a
-// device are fused into one multi-rank launch so their ring blocks are
-// co-resident (they spin on each other's flags).
+// Launch every pending plan.  By default a comm launches on the caller's
+// stream (stream order equals libmccs's bridge).  With bridge_streams = 1 it
+// launches on its own stream, bridged to the caller's with events like
+// libmccs (collectives.rs:86,134 + proxy/engine.rs:1185-1189).  Comms sharing
+// a device are fused into one multi-rank launch so their ring blocks are
+// co-resident (they spin on each other's flags); events join their streams
+// only when the callers used different ones.
 mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams) {
   std::map<int, std::vector<int>> by_dev;
   for (int i = 0; i < (int)comms.size(); ++i)
@@ -247,7 +258,10 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     Comm* c0 = comms[idx[0]];
     const bool bridge = c0->cfg.bridge_streams >= 0;
     hipStream_t st = bridge ? c0->stream : user_streams[idx[0]];
-    if (bridge || idx.size() > 1) {
+    bool one_user_stream = true;  // ranks sharing a GPU issued from one stream: no events needed
+    for (size_t k = 1; k < idx.size(); ++k) one_user_stream = one_user_stream && user_streams[idx[k]] == user_streams[idx[0]];
+    const bool events = bridge || !one_user_stream;
+    if (events) {
       for (size_t k = 0; k < idx.size(); ++k) {
         Comm* c = comms[idx[k]];
         MCCS_HIP(hipEventRecord(c->user_event, user_streams[idx[k]]));
@@ -276,7 +290,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       MCCS_HIP(hipLaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, 0, st));
     }
     MCCS_HIP(hipEventRecord(c0->event, st));
-    if (bridge || idx.size() > 1) {
+    if (events) {
       for (size_t k = 0; k < idx.size(); ++k) {
         if (!bridge && k == 0) continue;
         MCCS_HIP(hipStreamWaitEvent(user_streams[idx[k]], c0->event, 0));

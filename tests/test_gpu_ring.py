@@ -162,7 +162,7 @@ CONFIGS = [
     dict(buffer_size=1 << 20),
     dict(channel_count=2, rings="default", block_threads=544, lanes=1),  # reference profile
     dict(channel_count=5),
-    dict(bridge_streams=-1),
+    dict(bridge_streams=1),
 ]
 
 

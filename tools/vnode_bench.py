@@ -25,10 +25,12 @@ def main():
     ap.add_argument("--lanes", type=int, nargs="+", default=[0])
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--bridge", type=int, default=0, help="CommConfig.bridge_streams (0 = library default)")
     args = ap.parse_args()
     for n in args.n:
         for lanes in args.lanes:
-            comms = C.init_all([0] * n, C.CommConfig(lanes=lanes, block_threads=args.block))
+            comms = C.init_all([0] * n, C.CommConfig(lanes=lanes, block_threads=args.block,
+                                                          bridge_streams=args.bridge or None))
             for mib in args.sizes_mib:
                 cnt = (mib << 20) // 4
                 xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
@@ -51,7 +53,7 @@ def main():
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / args.iters
                 print(json.dumps({"n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels,
-                                  "block": comms[0].block_threads, "MiB": mib, "ms": round(dt * 1e3, 3),
+                                  "block": comms[0].block_threads, "bridge": args.bridge, "MiB": mib, "ms": round(dt * 1e3, 3),
                                   "algbw_GBps": round((mib << 20) / dt / 1e9, 2)}), flush=True)
                 del xs, ys
             torch.cuda.synchronize()
