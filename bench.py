@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size-mib", type=int, default=128)
     ap.add_argument("--dtype", default="float32", choices=["float32", "float16", "bfloat16"])
-    ap.add_argument("--jobs", default=None, choices=["setup2"],
+    ap.add_argument("--jobs", default=None, choices=["setup2", "setup2-interleaved"],
                     help="N>1: two concurrent allreduce jobs on the two halves of the node (BASELINE configs[4])")
     ap.add_argument("--variant", type=int, default=0, help="reduce main loop: 0 default, 1 REG, 2 LDS")
     ap.add_argument("--unroll", type=int, default=0)

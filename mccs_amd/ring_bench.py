@@ -195,8 +195,8 @@ def run(args):
     dev = torch.device("cuda", device)
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    if getattr(args, "jobs", None) == "setup2":
-        return run_setup2(args, torch, dist, C, rank, world, device, dev)
+    if getattr(args, "jobs", None) in ("setup2", "setup2-interleaved"):
+        return run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=args.jobs.endswith("interleaved"))
     exchange = _exchange_factory(dist, world)
 
     dt_name = args.dtype
@@ -279,16 +279,26 @@ def run(args):
     return out
 
 
-def run_setup2(args, torch, dist, C, rank, world, device, dev):
-    """BASELINE configs[4]: two concurrent AllReduce jobs, one per half of the
-    node (disjoint GPU sets), shapes from workloads/setup-2_{vgg,gpt_1}.toml.
-    Each job times its own K calls; both run at the same time."""
+def setup2_jobs(world: int, interleaved: bool) -> list[list[int]]:
+    """Global ranks of the two jobs: halves {0..n/2-1}/{n/2..n-1} (disjoint
+    GPU sets, no shared links) or even/odd ranks (rings share links)."""
     if world < 4 or world % 2:
-        raise SystemExit("--jobs setup2 needs an even world size >= 4")
-    half = world // 2
-    groups = [dist.new_group(list(range(0, half))), dist.new_group(list(range(half, world)))]
-    job = 0 if rank < half else 1
-    jrank = rank - job * half
+        raise ValueError("two concurrent jobs need an even world size >= 4")
+    if interleaved:
+        return [list(range(0, world, 2)), list(range(1, world, 2))]
+    return [list(range(0, world // 2)), list(range(world // 2, world))]
+
+
+def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False):
+    """BASELINE configs[4]: two concurrent AllReduce jobs on the node, shapes
+    from workloads/setup-2_{vgg,gpt_1}.toml.  Each job times its own K calls;
+    both run at the same time (traffic_gen/src/main.rs:167-228 reports each
+    job's per-iteration time the same way)."""
+    members = setup2_jobs(world, interleaved)
+    groups = [dist.new_group(m) for m in members]
+    job = 0 if rank in members[0] else 1
+    jrank = members[job].index(rank)
+    half = len(members[job])
     grp = groups[job]
     exchange = _subgroup_exchange(dist, grp, half)
     comm, mode = _make_validated_comm(torch, dist, C, jrank, half, device, dev, exchange, grp)
@@ -331,6 +341,7 @@ def run_setup2(args, torch, dist, C, rank, world, device, dev):
         "vs_baseline": None,
         "dtype": "f16",
         "data": "synthetic uniform[-1,1) per rank, device-resident buckets",
-        "config": {"workload": "2 concurrent allreduce jobs on disjoint GPU halves, setup-2 shapes "
-                               "(BASELINE configs[4])", "jobs": jobs, "fifo_mode": mode},
+        "config": {"workload": "2 concurrent allreduce jobs, setup-2 shapes (BASELINE configs[4]), "
+                               + ("interleaved ranks sharing links" if interleaved else "disjoint GPU halves"),
+                   "job_ranks": members, "jobs": jobs, "fifo_mode": mode},
     }
