@@ -198,6 +198,7 @@ def bench_reduce(args) -> dict:
         he.record(stream)
         torch.cuda.synchronize()
         hot_gbps = round(20 * 3 * n * esize / (hs.elapsed_time(he) / 1e3) / 1e9, 2)
+    calib = None if args.no_hot else hbm_calibration(sets, n, code, stream)
     tune = mccs_amd.get_tune()
     kernel_name = "reduce_lds_kernel" if tune["variant"] == 2 else "reduce_reg_kernel"
     tag = f"reduce_{args.dtype}_{args.size_mib}MiB_{kernel_name}"
@@ -221,6 +222,7 @@ def bench_reduce(args) -> dict:
                    "elements": n, "bytes_per_step": alg_bytes,
                    "buffer_sets_rotated": nsets,
                    "same_buffer_GBps": hot_gbps,
+                   "hbm_calibration": calib,
                    "reduce_tune": tune},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
@@ -229,6 +231,32 @@ def bench_reduce(args) -> dict:
         "wall_s": round(wall, 4),
     }
     return out
+
+
+def hbm_calibration(sets, n, code, stream) -> dict:
+    """What the same chip streams on simpler mixes, same buffers and rotation:
+    a 1:1 copy through the same kernel (1 source -> 1 destination).  Context
+    for roofline.frac (the reduce's 2:1 read/write mix streams at the copy's
+    rate), not a measurement of the reduce."""
+    import torch
+
+    import mccs_amd
+
+    def timed(fn, reps=20):
+        for i in range(3):
+            fn(i)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for i in range(reps):
+            fn(i)
+        e.record(stream)
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps / 1e3
+
+    nb = sets[0][0].numel() * sets[0][0].element_size()
+    t_copy = timed(lambda i: mccs_amd.reduce(sets[i % len(sets)][2], [sets[i % len(sets)][0]], count=n, dtype=code,
+                                             stream=stream))
+    return {"copy_1to1_GBps": round(2 * nb / t_copy / 1e9, 1)}
 
 
 def sweep_variants(sets, n, code, stream, reg_only=False):

@@ -246,7 +246,7 @@ struct ReduceTune {
   int variant = MCCS_REDUCE_VARIANT_REG;
   int unroll = 4;
   int policy = 1;  // 1 = non-temporal loads+stores
-  int blocks_per_cu = 16;
+  int blocks_per_cu = 32;  // 32 x 256-thread blocks per CU: one 16 KiB tile per block at 128 MiB (sweeps: +1-2 % over 16)
   int stages = 3;
   int waves = 4;
 };
@@ -372,7 +372,7 @@ static hipError_t dispatch(const ReduceArgs& a, hipStream_t st) {
   const bool reg = t.variant == MCCS_REDUCE_VARIANT_REG || t.variant == MCCS_REDUCE_VARIANT_REG_BLOCKED;
   const int map = t.variant == MCCS_REDUCE_VARIANT_REG_BLOCKED ? 1 : 0;
   const int unroll = reg ? t.unroll : 4;
-  const int bpc = reg ? t.blocks_per_cu : 16;
+  const int bpc = reg ? t.blocks_per_cu : 32;
   const int64_t npack = a.count / PACK;
   const int64_t tile = 256LL * unroll;
   int64_t tiles = (npack + tile - 1) / tile;
@@ -451,7 +451,7 @@ extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy
   const bool reg = t.variant != MCCS_REDUCE_VARIANT_LDS;
   t.unroll = unroll ? unroll : (reg ? 4 : 2);
   t.policy = policy < 0 ? d.policy : (reg ? policy : (policy ? 1 : 0));
-  t.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : (reg ? 16 : 1);
+  t.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : (reg ? 32 : 1);
   t.stages = stages ? stages : d.stages;
   t.waves = waves ? waves : d.waves;
   if (!reg && t.waves * t.stages * 2 * t.unroll > 160) return mccsInvalidArgument;
