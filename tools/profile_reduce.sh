@@ -10,7 +10,7 @@ OUT=$R/gpurun_out
 TAG=${PROF_TAG:-reduce}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline "$@")
+BENCH=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-hot "$@")  # --no-hot: no same-buffer / copy-calibration launches of the same kernel
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_${TAG}_trace" -o trace \
   -- "${BENCH[@]}" > "$OUT/prof_${TAG}_trace.log" 2>&1 || { echo "trace pass failed $?"; exit 3; }
 for C in FETCH_SIZE WRITE_SIZE; do
