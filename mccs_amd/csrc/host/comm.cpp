@@ -87,6 +87,11 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
   k.fence_mode = c->all_uncached ? MCCS_FENCE_UNCACHED : MCCS_FENCE_SYSTEM;
   const int tmo = c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms;
   k.timeout_ticks = tmo < 0 ? 0 : (uint64_t)tmo * 100000ull;  // s_memrealtime: 100 MHz
+  // one 4-step slice per chunk (2 slices in flight per lane): one flag
+  // round trip and one drain per chunk instead of two; +6-27 % on the virtual
+  // node.  MCCS_SLICE_STEPS=2 restores the reference's SliceSteps.
+  k.slice_steps = ALLREDUCE_CHUNKSTEPS;
+  if (const char* v = std::getenv("MCCS_SLICE_STEPS")) k.slice_steps = std::atoi(v) == 2 ? 2 : 4;
   DeviceGuard g(c->device);
   MCCS_HIP(ring_set_device_cfg(k));
   return mccsSuccess;

@@ -157,10 +157,13 @@ __device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1,
     u32x4* y = (u32x4*)d1;
     const uint32_t npack = (uint32_t)(nelem / PACK);
     const uint32_t wave = (uint32_t)tid >> 6, lane = (uint32_t)tid & 63;
-    const uint32_t per_iter = (uint32_t)nthr * U;  // packs
-    const uint32_t mine = wave * (64u * U) + lane;   // first pack of this lane in an iteration
-    uint32_t base = 0;
-    for (; base + per_iter <= npack; base += per_iter) {
+    // rows need whole waves: a partial last wave (e.g. the reference's 544 =
+    // 8.5 x 64 threads) sits out the vector loop and joins the scalar tail
+    const uint32_t nwaves = (uint32_t)nthr >> 6;
+    const uint32_t per_iter = nwaves * 64u * U;     // packs
+    const uint32_t mine = wave * (64u * U) + lane;  // first pack of this lane in an iteration
+    uint32_t base = wave < nwaves ? 0u : npack;  // npack: skip both vector passes
+    for (; wave < nwaves && base + per_iter <= npack; base += per_iter) {
       const uint32_t q = base + mine;
       u32x4 v[U];
 #pragma unroll

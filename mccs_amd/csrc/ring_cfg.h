@@ -30,7 +30,7 @@
 
 struct mccsRingKernelCfg {
   uint32_t fence_mode;    // MCCS_FENCE_*
-  uint32_t pad;
+  uint32_t slice_steps;   // FIFO steps per slice: 2 (reference SliceSteps) or 4 (one slice per chunk)
   uint64_t timeout_ticks; // s_memrealtime ticks (100 MHz); 0 = never
 };
 

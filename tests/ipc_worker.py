@@ -2,7 +2,9 @@
 """Multi-process (one rank per process) parity check through IPC-mapped FIFOs.
 
   python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
-      --master-port 29511 tools/ipc_check.py [--device-mod N]
+      --master-port 29511 tests/ipc_worker.py
+
+Driven by tests/test_gpu_ipc.py (a worker, not a test module).
 
 Every rank opens its peers' FIFO arenas with hipIpcOpenMemHandle (the
 multi-GPU bench path).  On a one-GPU box all ranks share cuda:0, which still

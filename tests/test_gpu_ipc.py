@@ -1,0 +1,34 @@
+"""GPU: ring AllReduce across processes through IPC-mapped FIFO arenas.
+
+Two ranks in two processes (tests/ipc_worker.py under torch.distributed.run),
+both on cuda:0 of the one-GPU box: exercises hipIpcGetMemHandle /
+hipIpcOpenMemHandle, the two-phase connect and cross-process flag hand-offs
+in both FIFO memory modes, bit for bit against the oracle.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_process_ring_matches_oracle():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(HERE, "ipc_worker.py")]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=os.path.dirname(HERE))
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(lines[-1])
+    assert res["all_ok"], res

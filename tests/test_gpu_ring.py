@@ -283,3 +283,40 @@ def test_baseline_sizes_exact(code, mib):
             assert torch.equal(recv[r], exp), f"rank {r}"
     finally:
         vnode.destroy(comms)
+
+
+def test_reference_slicing_matches_oracle(orc, monkeypatch):
+    """MCCS_SLICE_STEPS=2: the reference's two 2-step slices per chunk
+    (prims_simple.h SliceSteps) instead of the default one 4-step slice; the
+    FIFO then holds 4 slices in flight.  Elementwise results cannot depend on
+    slicing: still bit-exact."""
+    monkeypatch.setenv("MCCS_SLICE_STEPS", "2")
+    n = 4
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(44)
+        for count in (7, 300007, (3 << 20) + 5):
+            inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
+            outs = vnode.run_allreduce(comms, inputs, F16, 0)
+            exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0])
+            _check_all_equal(outs, exp, F16)
+    finally:
+        vnode.destroy(comms)
+        monkeypatch.delenv("MCCS_SLICE_STEPS")
+        C.init_all([0])[0].destroy()  # re-arm the device config with the default slicing
+
+
+@pytest.mark.parametrize("block", [96, 160, 544])
+def test_partial_wave_blocks(orc, block):
+    """Blocks that are not whole 64-lane waves (the reference's nWarps*32
+    sizes: 96 and 544 threads) on slices spanning several row iterations."""
+    n = 4
+    comms = C.init_all([0] * n, C.CommConfig(block_threads=block, lanes=2))
+    try:
+        rng = np.random.default_rng(block)
+        inputs = [vnode.gen(F32, (3 << 20) + 5, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, F32, 0)
+        exp = vnode.expected_allreduce(orc, inputs, F32, 0, comms[0])
+        _check_all_equal(outs, exp, F32)
+    finally:
+        vnode.destroy(comms)
