@@ -183,15 +183,22 @@ def init_communicator_rank(rank: int, nranks: int, device: int, exchange, config
     hsize = lib.mccsConnectHandleSize()
     mine = (ctypes.c_char * hsize)()
     h = ctypes.c_void_p()
-    _lib.check(lib.mccsCommSetupRank(ctypes.byref(h), rank, nranks, device, ctypes.byref(cfg), mine),
-               "mccsCommSetupRank")
+    rc = lib.mccsCommSetupRank(ctypes.byref(h), rank, nranks, device, ctypes.byref(cfg), mine)
     del keep
-    allh = exchange(bytes(mine))
+    # every rank joins the exchange even after a local failure (an empty
+    # handle), so a peer's error never leaves the others blocked in it
+    allh = exchange(bytes(mine) if rc == 0 else b"")
+    _lib.check(rc, "mccsCommSetupRank")
+    comm = Communicator(h.value)
     if len(allh) != nranks or any(len(x) != hsize for x in allh):
-        raise RuntimeError("connect-handle exchange returned malformed data")
+        comm.destroy()
+        raise RuntimeError("connect-handle exchange: a peer failed mccsCommSetupRank or sent malformed data")
     buf = ctypes.create_string_buffer(b"".join(allh), hsize * nranks)
-    _lib.check(lib.mccsCommConnect(h, buf), "mccsCommConnect")
-    return Communicator(h.value)
+    rc = lib.mccsCommConnect(h, buf)
+    if rc != 0:
+        comm.destroy()
+        _lib.check(rc, "mccsCommConnect")
+    return comm
 
 
 def all_reduce(comm: Communicator, send_buf, recv_buf, size: int, data_type=AllReduceDataType.Float32,

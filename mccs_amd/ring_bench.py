@@ -93,7 +93,15 @@ def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, gro
     attempts = [("uncached-fifo", C.CommConfig(timeout_ms=60000)),
                 ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000))]
     for name, cfg in attempts:
-        comm = C.init_communicator_rank(rank, world, device, exchange, cfg)
+        try:
+            comm = C.init_communicator_rank(rank, world, device, exchange, cfg)
+        except Exception as e:  # noqa: BLE001  (e.g. IPC refuses this memory kind: try the next mode)
+            print(f"[rank {rank}] {name}: init failed: {e}", flush=True)
+            comm = None
+        if not agree(dist, comm is not None, group):
+            if comm is not None:
+                comm.destroy()
+            continue
         nv = (4 << 20) // 4  # 4 MiB exact-sum fp32 check (multi-loop, ragged chunks)
         xv = _exact_inputs(torch, nv, rank, dev)
         yv = torch.empty_like(xv)

@@ -35,7 +35,8 @@ def _worker(rank, world, port, q):
         mx = ring_bench.max_over_ranks(dist, float(rank) + 0.5)
         # ring allreduce with gloo as the link: rank r holds its chunk sums
         ring_ok = _gloo_ring_allreduce(dist, rank, world)
-        q.put((rank, ok_exchange, all_true, one_false, mx, ring_ok))
+        init_ok = _init_failure_is_collective(dist, rank, world)
+        q.put((rank, ok_exchange, all_true, one_false, mx, ring_ok and init_ok))
     finally:
         dist.destroy_process_group()
 
@@ -83,6 +84,24 @@ def _gloo_ring_allreduce(dist, rank, world):
     # oracle: 1 channel, 160 threads -> 256-element (1 KiB) granule = rcs
     exp = orc.ring_allreduce(7, 0, xs, nchannels=1, nthreads=160, buff_size=1 << 22)
     return bool(np.array_equal(out.numpy().view(np.uint32), exp.view(np.uint32)))
+
+
+def _init_failure_is_collective(dist, rank, world):
+    """Without a GPU every rank's mccsCommSetupRank fails; each must still
+    join the handle exchange and then raise, so no rank blocks in it."""
+    import ctypes
+
+    from mccs_amd import _lib, ring_bench
+    from mccs_amd import comm as C
+
+    n = ctypes.c_int(0)
+    if ctypes.CDLL("libamdhip64.so").hipGetDeviceCount(ctypes.byref(n)) == 0 and n.value > 0:
+        return True  # a GPU is present: the failure path is not reachable here
+    try:
+        C.init_communicator_rank(rank, world, 0, ring_bench._exchange_factory(dist, world))
+    except (_lib.MccsError, RuntimeError):
+        return True
+    return False
 
 
 @pytest.mark.parametrize("world", [2])
