@@ -146,6 +146,11 @@ mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int *order);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
 const char *mccsGetErrorString(mccsResult_t r);
+/* Ring timing counters of `device` (armed by MCCS_RING_PROFILE=1 at
+ * communicator init): out4[0] slices, [1] ticks waiting for peer flags,
+ * [2] ticks streaming + draining (s_memrealtime, 100 MHz), [3] reserved.
+ * reset != 0 zeroes them after reading. */
+mccsResult_t mccs_ring_profile(int device, unsigned long long *out4, int reset);
 
 /* Host-only helpers (no GPU needed). */
 /* BASELINE configs[0] plumbing: the same ring schedule and FIFO protocol run

@@ -103,6 +103,7 @@ SIGNATURES: dict[str, tuple] = {
     "mccsCommInfo": (_c_int, [_c_void_p, _P(_c_int)]),
     "mccsCommRing": (_c_int, [_c_void_p, _c_int, _P(_c_int)]),
     "mccsCommDevComm": (_c_int, [_c_void_p, _P(_c_void_p)]),
+    "mccs_ring_profile": (_c_int, [_c_int, _P(ctypes.c_ulonglong), _c_int]),
     "mccsGetErrorString": (ctypes.c_char_p, [_c_int]),
     "mccs_default_rings": (_c_int, [_c_int, _c_int, _P(_c_int), _c_int]),
     "mccs_task_schema": (None, [_c_size_t, _c_int, _P(_c_int), _P(_c_int)]),

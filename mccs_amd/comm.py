@@ -249,6 +249,16 @@ def host_ring_allreduce(sendbufs, recvbufs, count: int, data_type, op_type=AllRe
     _lib.check(rc, "mccs_host_ring_allreduce")
 
 
+def ring_profile(device: int = 0, reset: bool = True) -> dict:
+    """Per-slice timing of the ring kernels on `device` (MCCS_RING_PROFILE=1
+    set before communicator init): slices, mean µs waiting for peer flags,
+    mean µs streaming + draining."""
+    out = (ctypes.c_ulonglong * 4)()
+    _lib.check(_sig().mccs_ring_profile(device, out, 1 if reset else 0), "mccs_ring_profile")
+    n = max(1, out[0])
+    return {"slices": out[0], "wait_us": out[1] / n / 100.0, "work_us": out[2] / n / 100.0}
+
+
 def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
     a, b = _ci(), _ci()
     _sig().mccs_task_schema(total_bytes, channels, ctypes.byref(a), ctypes.byref(b))
@@ -257,5 +267,5 @@ def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
 
 __all__ = ["AllReduceDataType", "AllReduceOpType", "CommConfig", "Communicator", "init_all",
            "init_communicator_rank", "all_reduce", "all_gather", "group", "default_rings", "task_schema",
-           "host_ring_allreduce",
+           "host_ring_allreduce", "ring_profile",
            "RedOp", "DataType"]

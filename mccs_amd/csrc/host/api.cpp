@@ -414,3 +414,13 @@ extern "C" int mccs_default_rings(int nranks, int nch_req, int* out, int max_cha
 extern "C" void mccs_task_schema(size_t total_bytes, int nch_cfg, int* nch, int* nthreads) {
   task_schema(total_bytes, nch_cfg, nch, nthreads);
 }
+
+// Ring profile counters of `device` (MCCS_RING_PROFILE=1 at communicator
+// init arms them): out[0] slices, out[1] wait ticks, out[2] work ticks
+// (s_memrealtime, 100 MHz), out[3] reserved.
+extern "C" mccsResult_t mccs_ring_profile(int device, unsigned long long* out4, int reset) {
+  if (!out4) return mccsInvalidArgument;
+  DeviceGuard g(device);
+  MCCS_HIP(ring_read_profile(out4, reset != 0));
+  return mccsSuccess;
+}

@@ -151,6 +151,7 @@ const void* ring_multi_kernel_ptr(int func, int dtype, int op);
 int coresident_ring_blocks(int block, int device);
 hipError_t ring_set_device_cfg(const mccsRingKernelCfg& cfg);
 hipError_t ring_take_device_error(unsigned* err);
+hipError_t ring_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_flush_caches(hipStream_t st);
 
 }  // namespace mccs

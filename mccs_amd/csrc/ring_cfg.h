@@ -32,7 +32,16 @@ struct mccsRingKernelCfg {
   uint32_t fence_mode;    // MCCS_FENCE_*
   uint32_t slice_steps;   // FIFO steps per slice: 2 (reference SliceSteps) or 4 (one slice per chunk)
   uint64_t timeout_ticks; // s_memrealtime ticks (100 MHz); 0 = never
+  uint32_t profile;       // 1: accumulate per-slice wait / work ticks (mccs_ring_profile)
+  uint32_t pad2;
 };
+
+// Per-device ring profile counters (s_memrealtime ticks, 100 MHz), summed
+// over every slice of every workgroup while mccsRingKernelCfg.profile is set.
+#define MCCS_PROF_SLICES 0  // slices executed
+#define MCCS_PROF_WAIT 1    // slice start -> peer flags satisfied (thread 0)
+#define MCCS_PROF_WORK 2    // flags satisfied -> stores drained, both barriers included
+#define MCCS_PROF_N 4
 
 // Multi-rank launch (several communicators of one device in ONE launch, used
 // when ranks share a GPU: tests' virtual node).  blockIdx.y = rank slot.

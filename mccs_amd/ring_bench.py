@@ -214,6 +214,9 @@ def run(args):
     nbytes = args.size_mib << 20
     n = nbytes // esize
 
+    # per-slice wait / stream timing on this rank's GPU (3 atomics per slice
+    # per workgroup): reported with the result to show where ring time goes
+    os.environ.setdefault("MCCS_RING_PROFILE", "1")
     comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange)
 
     g = torch.Generator(device=dev)
@@ -226,7 +229,9 @@ def run(args):
         C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, stream)
 
     K = args.steps
+    C.ring_profile(device, reset=True)
     elapsed = max_over_ranks(dist, _time_steps(torch, dist, comm, step, args.warmup, K))
+    prof = C.ring_profile(device, reset=True)
     per_step = elapsed / K
     del x, y
     full_ok = agree(dist, _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev))
@@ -260,6 +265,7 @@ def run(args):
                 "block_threads": comm.block_threads, "rings": rings, "fifo_mode": mode,
                 "validated_exact_sum_4MiB": True, "validated_exact_sum_full_size": full_ok,
                 "busbw_GBps": round(busbw, 3), "parallelism": f"ring{world}",
+                "rank0_slice_profile": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()},
                 # ranks sharing one GPU (a 1-GPU box): FIFO hand-offs stay in HBM, no xGMI link
                 "ranks_share_gpu": ndev < world,
             },

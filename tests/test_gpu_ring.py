@@ -320,3 +320,21 @@ def test_partial_wave_blocks(orc, block):
         _check_all_equal(outs, exp, F32)
     finally:
         vnode.destroy(comms)
+
+
+def test_ring_profile_counters(monkeypatch):
+    """MCCS_RING_PROFILE=1 arms the per-slice counters read by mccs_ring_profile."""
+    monkeypatch.setenv("MCCS_RING_PROFILE", "1")
+    comms = C.init_all([0] * 2)
+    try:
+        C.ring_profile(0, reset=True)
+        inputs = [np.ones(1 << 20, np.float32) for _ in range(2)]
+        outs = vnode.run_allreduce(comms, inputs, F32, 0)
+        assert all(np.all(o == 2.0) for o in outs)
+        p = C.ring_profile(0, reset=True)
+        assert p["slices"] > 0 and p["work_us"] > 0, p
+        assert C.ring_profile(0)["slices"] == 0
+    finally:
+        vnode.destroy(comms)
+        monkeypatch.delenv("MCCS_RING_PROFILE")
+        C.init_all([0])[0].destroy()  # disarm

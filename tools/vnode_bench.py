@@ -26,7 +26,10 @@ def main():
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bridge", type=int, default=0, help="CommConfig.bridge_streams (0 = library default)")
+    ap.add_argument("--profile", action="store_true", help="per-slice wait/stream timing (MCCS_RING_PROFILE)")
     args = ap.parse_args()
+    if args.profile:
+        os.environ["MCCS_RING_PROFILE"] = "1"
     for n in args.n:
         for lanes in args.lanes:
             comms = C.init_all([0] * n, C.CommConfig(lanes=lanes, block_threads=args.block,
@@ -45,6 +48,8 @@ def main():
                 for c in comms:
                     c.sync()
                 torch.cuda.synchronize()
+                if args.profile:
+                    C.ring_profile(0, reset=True)
                 t0 = time.perf_counter()
                 for _ in range(args.iters):
                     once()
@@ -52,9 +57,10 @@ def main():
                     c.sync()
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / args.iters
+                prof = C.ring_profile(0, reset=True) if args.profile else None
                 print(json.dumps({"n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels,
                                   "block": comms[0].block_threads, "bridge": args.bridge, "MiB": mib, "ms": round(dt * 1e3, 3),
-                                  "algbw_GBps": round((mib << 20) / dt / 1e9, 2)}), flush=True)
+                                  "algbw_GBps": round((mib << 20) / dt / 1e9, 2), "slice_profile": prof}), flush=True)
                 del xs, ys
             torch.cuda.synchronize()
             for c in comms:
