@@ -25,110 +25,6 @@ __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
   else *p = v;
 }
 
-// Block-cooperative reduce-copy of nelem elements, srcs/dsts already offset.
-// Runtime nsrcs in [1, MAXS], ndsts in [1, MAXD]. Threads [tid, nthr) of the
-// calling group participate. Used by the ring primitives (one workgroup per
-// channel lane) where nsrcs/ndsts vary per primitive call.
-// NTMASK: bit s set -> source s is read with non-temporal loads, which bypass
-// the CU's L1 (used for FIFO slots another workgroup rewrites between reads).
-template <int DT, int OP, int U, int MAXS, int MAXD, int LDPOL = kPlain, int STPOL = kPlain, int NTMASK = 0>
-__device__ __forceinline__ void reduce_copy_group(const void* const* srcs, int nsrcs,
-                                                  void* const* dsts, int ndsts, int64_t nelem,
-                                                  int tid, int nthr) {
-  using T = typename Elem<DT>::T;
-  constexpr int PACK = kPackElems<DT>;
-  if (nelem <= 0) return;
-  uintptr_t mis = 0;
-#pragma unroll
-  for (int s = 0; s < MAXS; ++s)
-    if (s < nsrcs) mis |= (uintptr_t)srcs[s];
-#pragma unroll
-  for (int d = 0; d < MAXD; ++d)
-    if (d < ndsts) mis |= (uintptr_t)dsts[d];
-  int64_t done = 0;
-  if ((mis & 15) == 0) {
-    const int64_t npack = nelem / PACK;
-    const int64_t step = (int64_t)nthr * U;
-    int64_t p = tid;
-    // full U-deep iterations: no bounds checks inside
-    for (; p + (int64_t)(U - 1) * nthr < npack; p += step) {
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        v[u] = ld16<(NTMASK & 1) ? kNonTemporal : LDPOL>((const u32x4*)srcs[0] + p + (int64_t)u * nthr);
-#pragma unroll
-      for (int s = 1; s < MAXS; ++s) {
-        if (s < nsrcs) {
-          u32x4 w[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-            w[u] = ((NTMASK >> s) & 1) ? ld16<kNonTemporal>((const u32x4*)srcs[s] + p + (int64_t)u * nthr)
-                                       : ld16<LDPOL>((const u32x4*)srcs[s] + p + (int64_t)u * nthr);
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[u] = pack_op<DT, OP>(v[u], w[u]);
-        }
-      }
-#pragma unroll
-      for (int d = 0; d < MAXD; ++d) {
-        if (d < ndsts) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) st16<STPOL>((u32x4*)dsts[d] + p + (int64_t)u * nthr, v[u]);
-        }
-      }
-    }
-    // remainder (< U packs per thread): one predicated U-deep pass, so every
-    // load is in flight at once instead of one memory round trip per pack
-    if (p < npack) {
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t q = p + (int64_t)u * nthr;
-        if (q < npack) v[u] = ld16<(NTMASK & 1) ? kNonTemporal : LDPOL>((const u32x4*)srcs[0] + q);
-      }
-#pragma unroll
-      for (int s = 1; s < MAXS; ++s) {
-        if (s < nsrcs) {
-          u32x4 w[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int64_t q = p + (int64_t)u * nthr;
-            if (q < npack)
-              w[u] = ((NTMASK >> s) & 1) ? ld16<kNonTemporal>((const u32x4*)srcs[s] + q)
-                                         : ld16<LDPOL>((const u32x4*)srcs[s] + q);
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (p + (int64_t)u * nthr < npack) v[u] = pack_op<DT, OP>(v[u], w[u]);
-        }
-      }
-#pragma unroll
-      for (int d = 0; d < MAXD; ++d) {
-        if (d < ndsts) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int64_t q = p + (int64_t)u * nthr;
-            if (q < npack) st16<STPOL>((u32x4*)dsts[d] + q, v[u]);
-          }
-        }
-      }
-    }
-    done = npack * PACK;
-  }
-  // typed scalar tail / unaligned fallback
-  for (int64_t e = done + tid; e < nelem; e += nthr) {
-    T v = (NTMASK & 1) ? __builtin_nontemporal_load((const T*)srcs[0] + e) : ((const T*)srcs[0])[e];
-#pragma unroll
-    for (int s = 1; s < MAXS; ++s)
-      if (s < nsrcs)
-        v = scalar_op<DT, OP>(v, ((NTMASK >> s) & 1) ? __builtin_nontemporal_load((const T*)srcs[s] + e)
-                                                     : ((const T*)srcs[s])[e]);
-#pragma unroll
-    for (int d = 0; d < MAXD; ++d)
-      if (d < ndsts) ((T*)dsts[d])[e] = v;
-  }
-}
-
-
 // Ring-step reduce-copy with the operand shape fixed at compile time (the
 // ring primitive knows it: NS sources, ND destinations) and a wave-contiguous
 // layout: wave w of the group owns U consecutive 1 KiB rows of each U*W KiB
