@@ -267,8 +267,8 @@ def sweep_variants(sets, n, code, stream, reg_only=False):
     import mccs_amd
 
     cfgs = []
-    if reg_only:  # REG: grid-strided (1) vs per-block contiguous (3) tiles, cache policy, grid size
-        for v in (1, 3):
+    if reg_only:  # REG: grid-strided (1) / per-block contiguous (3) tiles / wave rows (4), policy, grid
+        for v in (1, 3, 4):
             for u in (2, 4, 8):
                 for pol in (1, 2, 3):
                     for bpc in (8, 16, 32):

@@ -49,6 +49,7 @@ typedef enum {
 #define MCCS_REDUCE_VARIANT_REG 1 /* register streaming main loop */
 #define MCCS_REDUCE_VARIANT_LDS 2 /* LDS-DMA multi-stage staging main loop */
 #define MCCS_REDUCE_VARIANT_REG_BLOCKED 3 /* REG with a contiguous run of tiles per block */
+#define MCCS_REDUCE_VARIANT_REG_ROWS 4    /* REG with wave-contiguous 1 KiB rows */
 
 mccsResult_t mccs_hip_reduce(void *dst, const void *const *srcs, int nsrcs, size_t count, int dtype,
                              int op, hipStream_t stream);

@@ -42,8 +42,10 @@ struct ReduceArgs {
 
 // ---------------------------------------------------------------------------
 // REG: NS/ND > 0 are compile-time source/destination counts; 0 = runtime.
-// MAP 0: tiles grid-strided over blocks (the chip sweeps one contiguous window);
-// MAP 1: each block owns a contiguous run of tiles (2048+ independent streams).
+// MAP bit 0 clear: tiles grid-strided over blocks (the chip sweeps one
+// contiguous window); set: each block owns a contiguous run of tiles.
+// MAP bit 1: wave-contiguous rows (wave w reads U consecutive 1 KiB rows of
+// the tile) instead of block-strided packs (pack u of thread t at u*256+t).
 template <int DT, int OP, int NS, int ND, int U, int LDP, int STP, int MAP = 0>
 __global__ void __launch_bounds__(256) reduce_reg_kernel(ReduceArgs a) {
   using T = typename Elem<DT>::T;
@@ -57,23 +59,26 @@ __global__ void __launch_bounds__(256) reduce_reg_kernel(ReduceArgs a) {
   const int64_t tile = (int64_t)B * U;
   const int tid = threadIdx.x;
 
+  constexpr bool BLOCKED = MAP & 1, ROWS = MAP & 2;
+  constexpr int S = ROWS ? 64 : B;  // pack stride between a thread's U packs
+  const int lt = ROWS ? (tid >> 6) * 64 * U + (tid & 63) : tid;
   const int64_t ntiles = (npack + tile - 1) / tile;
-  const int64_t per = MAP ? (ntiles + gridDim.x - 1) / gridDim.x : 0;
-  const int64_t t0 = MAP ? (int64_t)blockIdx.x * per : blockIdx.x;
-  const int64_t t1 = MAP ? (t0 + per < ntiles ? t0 + per : ntiles) : ntiles;
-  const int64_t tstep = MAP ? 1 : gridDim.x;
+  const int64_t per = BLOCKED ? (ntiles + gridDim.x - 1) / gridDim.x : 0;
+  const int64_t t0 = BLOCKED ? (int64_t)blockIdx.x * per : blockIdx.x;
+  const int64_t t1 = BLOCKED ? (t0 + per < ntiles ? t0 + per : ntiles) : ntiles;
+  const int64_t tstep = BLOCKED ? 1 : gridDim.x;
   for (int64_t t = t0; t < t1; t += tstep) {
-    const int64_t base = t * tile + tid;
+    const int64_t base = t * tile + lt;
     if ((t + 1) * tile <= npack) {
       u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16<LDP>((const u32x4*)a.srcs[0] + base + u * B);
+      for (int u = 0; u < U; ++u) v[u] = ld16<LDP>((const u32x4*)a.srcs[0] + base + u * S);
 #pragma unroll
       for (int s = 1; s < MS; ++s) {
         if (s < nsrcs) {
           u32x4 w[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) w[u] = ld16<LDP>((const u32x4*)a.srcs[s] + base + u * B);
+          for (int u = 0; u < U; ++u) w[u] = ld16<LDP>((const u32x4*)a.srcs[s] + base + u * S);
 #pragma unroll
           for (int u = 0; u < U; ++u) v[u] = pack_op<DT, OP>(v[u], w[u]);
         }
@@ -82,13 +87,13 @@ __global__ void __launch_bounds__(256) reduce_reg_kernel(ReduceArgs a) {
       for (int d = 0; d < MD; ++d) {
         if (d < ndsts) {
 #pragma unroll
-          for (int u = 0; u < U; ++u) st16<STP>((u32x4*)a.dsts[d] + base + u * B, v[u]);
+          for (int u = 0; u < U; ++u) st16<STP>((u32x4*)a.dsts[d] + base + u * S, v[u]);
         }
       }
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t p = base + u * B;
+        const int64_t p = base + u * S;
         if (p < npack) {
           u32x4 v = ld16<LDP>((const u32x4*)a.srcs[0] + p);
 #pragma unroll
@@ -291,10 +296,15 @@ static hipError_t launch_reg(const ReduceArgs& a, int pol, int grid, hipStream_t
 template <int DT, int OP, int NS, int ND>
 static hipError_t launch_reg_u(const ReduceArgs& a, int u, int pol, int map, int grid, hipStream_t st) {
   if constexpr (tuned_grid<DT, OP>()) {
-    if (map) {
+    if (map == 1) {
       if (u == 2) return launch_reg<DT, OP, NS, ND, 2, 1>(a, pol, grid, st);
       if (u == 8) return launch_reg<DT, OP, NS, ND, 8, 1>(a, pol, grid, st);
       return launch_reg<DT, OP, NS, ND, 4, 1>(a, pol, grid, st);
+    }
+    if (map == 2) {
+      if (u == 2) return launch_reg<DT, OP, NS, ND, 2, 2>(a, pol, grid, st);
+      if (u == 8) return launch_reg<DT, OP, NS, ND, 8, 2>(a, pol, grid, st);
+      return launch_reg<DT, OP, NS, ND, 4, 2>(a, pol, grid, st);
     }
     if (u == 2) return launch_reg<DT, OP, NS, ND, 2, 0>(a, pol, grid, st);
     if (u == 8) return launch_reg<DT, OP, NS, ND, 8, 0>(a, pol, grid, st);
@@ -369,8 +379,8 @@ static hipError_t dispatch(const ReduceArgs& a, hipStream_t st) {
     if (ok) return e;
     // untuned (U,S,W) for this dtype/op: fall through to the REG loop
   }
-  const bool reg = t.variant == MCCS_REDUCE_VARIANT_REG || t.variant == MCCS_REDUCE_VARIANT_REG_BLOCKED;
-  const int map = t.variant == MCCS_REDUCE_VARIANT_REG_BLOCKED ? 1 : 0;
+  const bool reg = t.variant != MCCS_REDUCE_VARIANT_LDS;
+  const int map = t.variant == MCCS_REDUCE_VARIANT_REG_BLOCKED ? 1 : t.variant == MCCS_REDUCE_VARIANT_REG_ROWS ? 2 : 0;
   const int unroll = reg ? t.unroll : 4;
   const int bpc = reg ? t.blocks_per_cu : 32;
   const int64_t npack = a.count / PACK;
@@ -440,7 +450,7 @@ extern "C" mccsResult_t mccs_hip_reduce(void* dst, const void* const* srcs, int 
 
 extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu,
                                              int stages, int waves) {
-  if (variant < 0 || variant > MCCS_REDUCE_VARIANT_REG_BLOCKED) return mccsInvalidArgument;
+  if (variant < 0 || variant > MCCS_REDUCE_VARIANT_REG_ROWS) return mccsInvalidArgument;
   if (policy > 3) return mccsInvalidArgument;
   if (unroll < 0 || unroll > 8 || (unroll & (unroll - 1))) return mccsInvalidArgument;
   if (stages < 0 || stages == 1 || stages > 4 || waves < 0 || (waves != 0 && waves != 4 && waves != 8))
