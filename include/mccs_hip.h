@@ -153,6 +153,36 @@ const char *mccsGetErrorString(mccsResult_t r);
  * reset != 0 zeroes them after reading. */
 mccsResult_t mccs_ring_profile(int device, unsigned long long *out4, int reset);
 
+/* ----------------------------------------------------------------------
+ * Application <-> backend bridge (the reference's mCCS service model: the
+ * collectives run in a backend process; the application shares buffers and
+ * stream order with it through IPC handles).  Handles are the 64-byte
+ * hipIpcMemHandle_t / hipIpcEventHandle_t as opaque bytes.
+ * ---------------------------------------------------------------------- */
+#define MCCS_IPC_HANDLE_BYTES 64
+/* libmccs cuda_malloc (src/libmccs/src/memory.rs:12-37): the backend
+ * allocates and exports; the application opens the handle. */
+mccsResult_t mccsMemAllocShared(int device, size_t bytes, void **dptr, void *handle_out);
+mccsResult_t mccsMemFreeShared(int device, void *dptr);
+mccsResult_t mccsMemOpenShared(int device, const void *handle, void **dptr);
+mccsResult_t mccsMemCloseShared(int device, void *dptr);
+/* libmccs register_stream (communicator.rs:47-66): the application creates an
+ * interprocess event per stream; the backend opens it. */
+mccsResult_t mccsEventCreateShared(int device, void **event, void *handle_out);
+mccsResult_t mccsEventOpenShared(int device, const void *handle, void **event);
+mccsResult_t mccsEventDestroyShared(void *event);
+/* The comm's completion event (recorded after every launch) exported for the
+ * application (InitCommunicator's event handle, communicator.rs:35-38). */
+mccsResult_t mccsCommEventHandle(mccsComm_t comm, void *handle_out);
+/* The comm's own stream, and wait_user_event (proxy/engine.rs:1185-1189):
+ * the comm stream waits on an (opened) application event. */
+mccsResult_t mccsCommStream(mccsComm_t comm, hipStream_t *stream);
+mccsResult_t mccsCommWaitEvent(mccsComm_t comm, void *event);
+/* Application side of the bridge (collectives.rs:86,134): record the user
+ * event on its stream before a request; wait on the backend event after. */
+mccsResult_t mccsEventRecordShared(void *event, hipStream_t stream);
+mccsResult_t mccsStreamWaitShared(hipStream_t stream, void *event);
+
 /* Host-only helpers (no GPU needed). */
 /* BASELINE configs[0] plumbing: the same ring schedule and FIFO protocol run
  * by nranks x nchannels host threads over host memory (no GPU).  rings as in

@@ -104,6 +104,18 @@ SIGNATURES: dict[str, tuple] = {
     "mccsCommRing": (_c_int, [_c_void_p, _c_int, _P(_c_int)]),
     "mccsCommDevComm": (_c_int, [_c_void_p, _P(_c_void_p)]),
     "mccs_ring_profile": (_c_int, [_c_int, _P(ctypes.c_ulonglong), _c_int]),
+    "mccsMemAllocShared": (_c_int, [_c_int, _c_size_t, _P(_c_void_p), _c_void_p]),
+    "mccsMemFreeShared": (_c_int, [_c_int, _c_void_p]),
+    "mccsMemOpenShared": (_c_int, [_c_int, _c_void_p, _P(_c_void_p)]),
+    "mccsMemCloseShared": (_c_int, [_c_int, _c_void_p]),
+    "mccsEventCreateShared": (_c_int, [_c_int, _P(_c_void_p), _c_void_p]),
+    "mccsEventOpenShared": (_c_int, [_c_int, _c_void_p, _P(_c_void_p)]),
+    "mccsEventDestroyShared": (_c_int, [_c_void_p]),
+    "mccsCommEventHandle": (_c_int, [_c_void_p, _c_void_p]),
+    "mccsCommStream": (_c_int, [_c_void_p, _P(_c_void_p)]),
+    "mccsCommWaitEvent": (_c_int, [_c_void_p, _c_void_p]),
+    "mccsEventRecordShared": (_c_int, [_c_void_p, _c_void_p]),
+    "mccsStreamWaitShared": (_c_int, [_c_void_p, _c_void_p]),
     "mccsGetErrorString": (ctypes.c_char_p, [_c_int]),
     "mccs_default_rings": (_c_int, [_c_int, _c_int, _P(_c_int), _c_int]),
     "mccs_task_schema": (None, [_c_size_t, _c_int, _P(_c_int), _P(_c_int)]),

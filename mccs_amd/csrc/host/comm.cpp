@@ -213,7 +213,9 @@ mccsResult_t comm_alloc_local(Comm* c) {
   c->work_next = 0;
   c->work_acked_min = 0;
   MCCS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  MCCS_HIP(hipEventCreateWithFlags(&c->event, hipEventDisableTiming));
+  // interprocess: a backend process exports it to the application
+  // (InitCommunicator's event handle, libmccs communicator.rs:35-38)
+  MCCS_HIP(hipEventCreateWithFlags(&c->event, hipEventDisableTiming | hipEventInterprocess));
   MCCS_HIP(hipEventCreateWithFlags(&c->user_event, hipEventDisableTiming));
   c->sched.assign(c->nch, ChannelSchedule{});
   return mccsSuccess;
