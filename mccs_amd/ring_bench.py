@@ -91,7 +91,10 @@ def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, gro
     """Build the communicator; check an exact-sum fp32 AllReduce bit for bit
     on every rank; on failure rebuild with cached FIFOs + system fences."""
     attempts = [("uncached-fifo", C.CommConfig(timeout_ms=60000)),
-                ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000))]
+                ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000)),
+                ("sender-side-uncached-fifo", C.CommConfig(locality=C.LOCALITY_SENDER, timeout_ms=60000)),
+                ("sender-side-cached-fifo", C.CommConfig(locality=C.LOCALITY_SENDER, fifo_memory=C.FIFO_DEVICE,
+                                                         timeout_ms=60000))]
     for name, cfg in attempts:
         try:
             comm = C.init_communicator_rank(rank, world, device, exchange, cfg)
