@@ -170,11 +170,14 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   cfg->work_fifo_depth = 4096;
   cfg->bridge_streams = -1;
   // operator overrides (no rebuild needed): MCCS_LOCALITY=sender|receiver,
-  // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE
+  // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE,
+  // MCCS_BRIDGE_STREAMS, MCCS_FIFO_MEMORY=uncached|device
   if (const char* v = std::getenv("MCCS_LOCALITY"))
     cfg->locality = (v[0] == 's' || v[0] == 'S') ? MCCS_LOCALITY_SENDER : MCCS_LOCALITY_RECEIVER;
   if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BRIDGE_STREAMS")) cfg->bridge_streams = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_FIFO_MEMORY"))
+    cfg->fifo_memory = (v[0] == 'd' || v[0] == 'D') ? MCCS_FIFO_DEVICE : MCCS_FIFO_UNCACHED;
   if (const char* v = std::getenv("MCCS_BLOCK_THREADS")) cfg->block_threads = std::atoi(v);
   if (const char* v = std::getenv("MCCS_CHANNELS")) cfg->channel_count = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BUFFER_SIZE")) cfg->buffer_size = std::atoi(v);
