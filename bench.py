@@ -274,16 +274,14 @@ def sweep_variants(sets, n, code, stream, reg_only=False):
                     for bpc in (8, 16, 32):
                         cfgs.append((v, u, pol, bpc, 0, 0))
     else:
-        for u in (2, 4, 8):  # REG
-            for bpc in (4, 8, 16):
-                cfgs.append((1, u, 1, bpc, 0, 0))
-        for u, s, w in ((1, 2, 4), (1, 3, 4), (1, 4, 4), (2, 2, 4), (2, 3, 4), (2, 4, 4), (4, 2, 4),
-                        (4, 3, 4), (4, 4, 4), (1, 2, 8), (1, 3, 8), (1, 4, 8), (2, 2, 8), (2, 3, 8),
-                        (2, 4, 8), (4, 2, 8)):  # LDS
+        for u, bpc in ((4, 32), (4, 16), (8, 16)):  # REG
+            cfgs.append((1, u, 1, bpc, 0, 0))
+        for u, s, w in ((1, 3, 4), (2, 2, 4), (2, 3, 4), (4, 2, 4), (4, 3, 4), (4, 4, 4), (8, 2, 4),
+                        (4, 3, 5), (2, 3, 6), (4, 2, 6), (4, 3, 6), (1, 2, 8), (2, 2, 8), (4, 2, 8)):  # LDS
             for bpc in (1, 2):
                 if w * s * 2 * u * bpc <= 160:
                     cfgs.append((2, u, 1, bpc, s, w))
-        cfgs.append((2, 2, 0, 1, 3, 4))
+        cfgs.append((2, 4, 2, 1, 3, 4))  # plain LDS-DMA reads
         cfgs.append((1, 4, 0, 8, 0, 0))
     c0 = sets[0][2]
     alg = 3 * c0.numel() * c0.element_size()

@@ -57,8 +57,9 @@ mccsResult_t mccs_hip_reduce_copy(void *const *dsts, int ndsts, const void *cons
                                   size_t count, int dtype, int op, hipStream_t stream);
 /* Select the main loop (0 = default), unroll = KiB per source per wave tile
  * for LDS / 16-byte packs per lane for REG (1/2/4/8, 0 = default), cache
- * policy (0 plain, 1 non-temporal, -1 default; REG only: 2 nt loads + plain
- * stores, 3 plain loads + nt stores), persistent blocks per CU,
+ * policy (0 plain, 1 non-temporal, -1 default; REG: 2 nt loads + plain
+ * stores, 3 plain loads + nt stores; LDS: 2 plain LDS-DMA + nt stores),
+ * persistent blocks per CU,
  * LDS ring stages (2..4) and waves per block (4/8); 0 = default for each.
  * Process-wide; for benchmarking and tests. */
 mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu, int stages,

@@ -17,6 +17,7 @@
 //        with ds_read_b128, applies the op and stores.  Bytes in flight are
 //        bounded by LDS (160 KiB/CU) instead of VGPRs.
 // Grid: persistent, blocks_per_cu * 256 CUs, grid-stride over tiles.
+// Default: LDS with nt DMA reads (the fastest from HBM).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -144,7 +145,7 @@ __device__ __forceinline__ void wait_younger(int nd, int ns) {
   static_assert(S >= 2 && S <= 4, "stages");
   static_assert((S - 1) * (G + U) < 64, "vmcnt range");
 #define MCCS_WY(ND, NS) \
-  case (ND) * 4 + (NS): wait_vmcnt<(ND) * G + (NS) * U>(); break;
+  case (ND) * 4 + (NS): wait_vmcnt<((ND) < S && (NS) < S) ? (ND) * G + (NS) * U : 0>(); break;
   switch (nd * 4 + ns) {
     MCCS_WY(0, 0) MCCS_WY(0, 1) MCCS_WY(0, 2) MCCS_WY(0, 3)
     MCCS_WY(1, 0) MCCS_WY(1, 1) MCCS_WY(1, 2) MCCS_WY(1, 3)
@@ -156,20 +157,33 @@ __device__ __forceinline__ void wait_younger(int nd, int ns) {
 }
 
 // One lane's 16 bytes of a wave-wide LDS-DMA: LDS dst = M0 + lane*16.
+// NT: non-temporal (streaming) policy on the DMA read.
+template <bool NT>
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_wave_base) {
   uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_wave_base)
-      : "memory");
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_wave_base)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_wave_base)
+        : "memory");
 }
 
-template <int DT, int OP, int U, int S, int W, int STP>
+template <int DT, int OP, int U, int S, int W, int LDP, int STP>
 __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
   constexpr int PACK = kPackElems<DT>;
   constexpr int G = 2 * U;        // LDS-DMA instructions per wave tile (2 sources)
@@ -194,8 +208,8 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
     for (int u = 0; u < U; ++u) {
       int64_t p = tile * wtile + u * 64 + lane;
       p = p < npack ? p : npack - 1;  // clamp: partial last tile re-reads a valid pack
-      glds16(s0 + p, base + u * 1024);
-      glds16(s1 + p, base + (U + u) * 1024);
+      glds16<LDP == kNonTemporal>(s0 + p, base + u * 1024);
+      glds16<LDP == kNonTemporal>(s1 + p, base + (U + u) * 1024);
     }
   };
 
@@ -242,16 +256,16 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
 // ---------------------------------------------------------------------------
 // Run-time configuration (process-wide; set before launches).  Defaults are
 // the fastest measured on MI355X with inputs streamed from HBM (bench.py
-// --sweep with buffer rotation, profiles/r01_*): REG main loop, 4 packs per
-// source per lane, 16 blocks of 256 per CU, non-temporal loads and stores
-// (6.39 TB/s).  The LDS-DMA loop (U=2, 3 stages, 4 waves, 1 block/CU) is
-// faster only when the inputs are Infinity-Cache resident (7.27 vs 6.59
-// TB/s same-buffer) and slower from HBM (5.92 TB/s); see DESIGN.md.
+// --sweep with buffer rotation, profiles/r01_*): the LDS-DMA loop with
+// non-temporal DMA reads and stores, 4 KiB per source per wave tile, a
+// 3-stage ring (double buffering plus one tile of slack), 4 waves, one block
+// per CU: 6.52 TB/s against 6.43 for the best REG loop on the same box.
+// Without nt on the DMA reads the same loop streams 5.9 TB/s; see DESIGN.md.
 struct ReduceTune {
-  int variant = MCCS_REDUCE_VARIANT_REG;
-  int unroll = 4;
-  int policy = 1;  // 1 = non-temporal loads+stores
-  int blocks_per_cu = 32;  // 32 x 256-thread blocks per CU: one 16 KiB tile per block at 128 MiB (sweeps: +1-2 % over 16)
+  int variant = MCCS_REDUCE_VARIANT_LDS;
+  int unroll = 4;  // LDS: 4 KiB per source per wave tile
+  int policy = 1;  // 1 = non-temporal LDS-DMA reads + nt stores
+  int blocks_per_cu = 1;  // LDS: one 4-wave block per CU (96 KiB of LDS ring)
   int stages = 3;
   int waves = 4;
 };
@@ -319,12 +333,15 @@ template <int DT, int OP, int U, int S, int W>
 static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t st) {
   static_assert(lds_fits<U, S, W>(), "LDS budget");
   const size_t lds = (size_t)W * S * 2 * U * 1024;
-  auto kn = reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal>;
-  auto kp = reduce_lds_kernel<DT, OP, U, S, W, kPlain>;
+  // pol: 0 plain DMA + plain stores, 1 nt DMA + nt stores, 2 plain DMA + nt stores
+  auto kn = reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNonTemporal>;
+  auto kp = reduce_lds_kernel<DT, OP, U, S, W, kPlain, kPlain>;
+  auto ks = reduce_lds_kernel<DT, OP, U, S, W, kPlain, kNonTemporal>;
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load(std::memory_order_relaxed)) {
     (void)hipFuncSetAttribute((const void*)kn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)hipFuncSetAttribute((const void*)kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set.store(true, std::memory_order_relaxed);
   }
   constexpr int PACK = kPackElems<DT>;
@@ -333,8 +350,10 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
   int64_t blocks = (wtiles + W - 1) / W;
   const int64_t gmax = (int64_t)num_cus() * bpc;
   const int grid = (int)(blocks < gmax ? (blocks > 0 ? blocks : 1) : gmax);
-  if (pol)
+  if (pol == 1)
     hipLaunchKernelGGL(kn, dim3(grid), dim3(W * 64), lds, st, a);
+  else if (pol == 2)
+    hipLaunchKernelGGL(ks, dim3(grid), dim3(W * 64), lds, st, a);
   else
     hipLaunchKernelGGL(kp, dim3(grid), dim3(W * 64), lds, st, a);
   return hipGetLastError();
@@ -347,12 +366,11 @@ static hipError_t launch_lds_cfg(const ReduceArgs& a, const ReduceTune& t, bool*
   *ok = true;
 #define MCCS_LDS(U, S, W) \
   if (t.unroll == U && t.stages == S && t.waves == W) return launch_lds<DT, OP, U, S, W>(a, t.policy, t.blocks_per_cu, st);
-  MCCS_LDS(2, 3, 4)
+  MCCS_LDS(4, 3, 4)
   if constexpr (OP == OpSum && (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16)) {
-    MCCS_LDS(1, 2, 4) MCCS_LDS(1, 3, 4) MCCS_LDS(1, 4, 4) MCCS_LDS(2, 2, 4) MCCS_LDS(2, 4, 4)
-    MCCS_LDS(4, 2, 4) MCCS_LDS(4, 3, 4) MCCS_LDS(4, 4, 4)
-    MCCS_LDS(1, 2, 8) MCCS_LDS(1, 3, 8) MCCS_LDS(1, 4, 8) MCCS_LDS(2, 2, 8) MCCS_LDS(2, 3, 8)
-    MCCS_LDS(2, 4, 8) MCCS_LDS(4, 2, 8)
+    MCCS_LDS(1, 3, 4) MCCS_LDS(2, 2, 4) MCCS_LDS(2, 3, 4) MCCS_LDS(4, 2, 4) MCCS_LDS(4, 4, 4) MCCS_LDS(8, 2, 4)
+    MCCS_LDS(4, 3, 5) MCCS_LDS(2, 3, 6) MCCS_LDS(4, 2, 6) MCCS_LDS(4, 3, 6)
+    MCCS_LDS(1, 2, 8) MCCS_LDS(2, 2, 8) MCCS_LDS(4, 2, 8)
   }
 #undef MCCS_LDS
   *ok = false;
@@ -453,14 +471,14 @@ extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy
   if (variant < 0 || variant > MCCS_REDUCE_VARIANT_REG_ROWS) return mccsInvalidArgument;
   if (policy > 3) return mccsInvalidArgument;
   if (unroll < 0 || unroll > 8 || (unroll & (unroll - 1))) return mccsInvalidArgument;
-  if (stages < 0 || stages == 1 || stages > 4 || waves < 0 || (waves != 0 && waves != 4 && waves != 8))
+  if (stages < 0 || stages == 1 || stages > 4 || waves < 0 || (waves != 0 && (waves < 4 || waves > 8 || waves == 7)))
     return mccsInvalidArgument;
   ReduceTune d;
   ReduceTune t;
   t.variant = variant ? variant : d.variant;
   const bool reg = t.variant != MCCS_REDUCE_VARIANT_LDS;
-  t.unroll = unroll ? unroll : (reg ? 4 : 2);
-  t.policy = policy < 0 ? d.policy : (reg ? policy : (policy ? 1 : 0));
+  t.unroll = unroll ? unroll : 4;
+  t.policy = policy < 0 ? d.policy : (reg ? policy : (policy == 3 ? 1 : policy));
   t.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : (reg ? 32 : 1);
   t.stages = stages ? stages : d.stages;
   t.waves = waves ? waves : d.waves;
