@@ -87,9 +87,10 @@ def _subgroup_exchange(dist, group, n):
     return exchange
 
 
-def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, group=None):
+def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, group=None, full=None):
     """Build the communicator; check an exact-sum fp32 AllReduce bit for bit
-    on every rank; on failure rebuild with cached FIFOs + system fences."""
+    on every rank (and, with full=(n, torch dtype, AllReduceDataType), one at
+    the timed size and dtype); on failure rebuild with the next FIFO mode."""
     attempts = [("uncached-fifo", C.CommConfig(timeout_ms=60000)),
                 ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000)),
                 ("sender-side-uncached-fifo", C.CommConfig(locality=C.LOCALITY_SENDER, timeout_ms=60000)),
@@ -114,6 +115,9 @@ def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, gro
             comm.sync()
             torch.cuda.synchronize()
             ok = bool(torch.equal(yv, _expected_exact(torch, nv, world, dev)))
+            del xv, yv
+            if ok and full is not None:
+                ok = _full_size_exact(torch, C, comm, rank, world, full[0], full[1], full[2], dev)
         except Exception as e:  # noqa: BLE001  (watchdog / HIP error: try the next mode)
             print(f"[rank {rank}] {name}: {e}", flush=True)
             ok = False
@@ -220,7 +224,7 @@ def run(args):
     # per-slice wait / stream timing on this rank's GPU (3 atomics per slice
     # per workgroup): reported with the result to show where ring time goes
     os.environ.setdefault("MCCS_RING_PROFILE", "1")
-    comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange)
+    comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, full=(n, tdt, code))
 
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
@@ -266,7 +270,8 @@ def run(args):
                             f"buckets, chunked FIFO pipeline ({WORKLOADS.get((dt_name, args.size_mib), 'custom')})",
                 "bytes_per_rank": nbytes, "channels": comm.nchannels, "lanes": comm.lanes,
                 "block_threads": comm.block_threads, "rings": rings, "fifo_mode": mode,
-                "validated_exact_sum_4MiB": True, "validated_exact_sum_full_size": full_ok,
+                "validated_exact_sum_4MiB": True, "validated_exact_sum_full_size_before_timing": True,
+                "validated_exact_sum_full_size_after_timing": full_ok,
                 "busbw_GBps": round(busbw, 3), "parallelism": f"ring{world}",
                 "rank0_slice_profile": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()},
                 # ranks sharing one GPU (a 1-GPU box): FIFO hand-offs stay in HBM, no xGMI link
@@ -318,8 +323,9 @@ def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False
     half = len(members[job])
     grp = groups[job]
     exchange = _subgroup_exchange(dist, grp, half)
-    comm, mode = _make_validated_comm(torch, dist, C, jrank, half, device, dev, exchange, grp)
     name, n = SETUP2_JOBS[job]
+    comm, mode = _make_validated_comm(torch, dist, C, jrank, half, device, dev, exchange, grp,
+                                      full=(n, torch.float16, C.AllReduceDataType.Float16))
     g = torch.Generator(device=dev)
     g.manual_seed(2000 + rank)
     x = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(torch.float16)
