@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of reduce variants (stderr)")
     ap.add_argument("--sweep-reg", action="store_true", help="interleaved A/B of the REG loop's map/policy/grid")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="N>1: skip the on-node choice of FIFO placement / lanes (library defaults + fallbacks)")
     ap.add_argument("--no-hot", action="store_true", help="skip the same-buffer measurement (profiling)")
     return ap.parse_args()
 

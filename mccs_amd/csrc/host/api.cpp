@@ -333,7 +333,7 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
   if (!c) return mccsInvalidArgument;
   DeviceGuard g(c->device);
   MCCS_HIP(hipEventSynchronize(c->event));
-  MCCS_HIP(hipStreamSynchronize(c->stream));
+  if (c->stream) MCCS_HIP(hipStreamSynchronize(c->stream));
   unsigned err = 0;
   MCCS_HIP(ring_take_device_error(&err));
   uint32_t abort_val = 0;

@@ -212,10 +212,9 @@ mccsResult_t comm_alloc_local(Comm* c) {
   c->chan_next.assign(c->nch, 0);
   c->work_next = 0;
   c->work_acked_min = 0;
-  MCCS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  // interprocess: a backend process exports it to the application
-  // (InitCommunicator's event handle, libmccs communicator.rs:35-38)
-  MCCS_HIP(hipEventCreateWithFlags(&c->event, hipEventDisableTiming | hipEventInterprocess));
+  // comm stream: created on first use (comm_stream); the event becomes
+  // interprocess only when a backend exports it (comm_make_event_ipc)
+  MCCS_HIP(hipEventCreateWithFlags(&c->event, hipEventDisableTiming));
   MCCS_HIP(hipEventCreateWithFlags(&c->user_event, hipEventDisableTiming));
   c->sched.assign(c->nch, ChannelSchedule{});
   return mccsSuccess;
@@ -272,6 +271,31 @@ mccsResult_t comm_build_device(Comm* c) {
   MCCS_HIP(hipMemcpy(c->d_comm, &hc, sizeof(hc), hipMemcpyHostToDevice));
   MCCS_CHECK(comm_set_kernel_cfg(c));
   c->connected = true;
+  return mccsSuccess;
+}
+
+mccsResult_t comm_stream(Comm* c, hipStream_t* out) {
+  if (!c->stream) {
+    DeviceGuard g(c->device);
+    MCCS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  }
+  *out = c->stream;
+  return mccsSuccess;
+}
+
+// InitCommunicator's event handle (libmccs communicator.rs:35-38): a backend
+// process exports the comm event to the application, so it must be an
+// interprocess event.  Pending work is drained first, so the new event is
+// recorded after every later launch and no earlier one is lost.
+mccsResult_t comm_make_event_ipc(Comm* c) {
+  if (c->event_ipc) return mccsSuccess;
+  DeviceGuard g(c->device);
+  MCCS_HIP(hipEventSynchronize(c->event));
+  hipEvent_t e = nullptr;
+  MCCS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess));
+  (void)hipEventDestroy(c->event);
+  c->event = e;
+  c->event_ipc = true;
   return mccsSuccess;
 }
 

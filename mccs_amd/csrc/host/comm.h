@@ -124,8 +124,14 @@ struct Comm {
   uint32_t work_next = 0;      // work_queue_next_available
   uint32_t work_acked_min = 0; // work_queue_acked_min
   std::vector<uint32_t> chan_next;  // per channel work_queue_next_available
+  // The comm stream (libmccs two-stream bridge) and the interprocess flavour
+  // of the comm event are created on first need: a stream a process never
+  // uses costs nothing, but every queue a process activates competes for the
+  // GPU's hardware queues (ranks sharing one GPU measured 0.40 -> 0.62 ms
+  // per 64 MiB AllReduce after one extra active queue per process).
   hipStream_t stream = nullptr;
   hipEvent_t event = nullptr;       // comm -> user
+  bool event_ipc = false;           // event created with hipEventInterprocess
   hipEvent_t user_event = nullptr;  // user -> comm
   bool connected = false;
   bool failed = false;
@@ -142,6 +148,8 @@ mccsResult_t comm_build_device(Comm* c);
 void default_rings(int nranks, int nch_req, std::vector<std::vector<int>>* rings);
 mccsResult_t comm_free(Comm* c);
 mccsResult_t comm_set_kernel_cfg(Comm* c);
+mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream on first use
+mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one
 // plan.cpp
 mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count);
 mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams);

@@ -132,7 +132,7 @@ static mccsResult_t wait_work_queue(Comm* c, uint32_t target) {
       if (ackd[ch] == c->chan_next[ch]) __atomic_store_n(&c->h_done[ch], all, __ATOMIC_RELAXED);
     c->work_acked_min = all;
     if (!rolling_less_u32(c->work_acked_min + c->work_depth, target)) return mccsSuccess;
-    if ((spins & 0xfffff) == 0xfffff && hipStreamQuery(c->stream) == hipSuccess) {
+    if ((spins & 0xfffff) == 0xfffff && hipEventQuery(c->event) == hipSuccess) {
       // stream idle but acks missing: the kernel aborted
       return mccsRemoteError;
     }
@@ -257,7 +257,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work(comms[idx[k]], &lds[k]));
     Comm* c0 = comms[idx[0]];
     const bool bridge = c0->cfg.bridge_streams >= 0;
-    hipStream_t st = bridge ? c0->stream : user_streams[idx[0]];
+    hipStream_t st = user_streams[idx[0]];
+    if (bridge) MCCS_CHECK(comm_stream(c0, &st));
     bool one_user_stream = true;  // ranks sharing a GPU issued from one stream: no events needed
     for (size_t k = 1; k < idx.size(); ++k) one_user_stream = one_user_stream && user_streams[idx[k]] == user_streams[idx[0]];
     const bool events = bridge || !one_user_stream;

@@ -92,6 +92,7 @@ extern "C" mccsResult_t mccsCommEventHandle(mccsComm_t comm, void* handle_out) {
   Comm* c = (Comm*)comm;
   if (!c || !handle_out) return mccsInvalidArgument;
   DeviceGuard g(c->device);
+  MCCS_CHECK(comm_make_event_ipc(c));
   hipIpcEventHandle_t h;
   MCCS_HIP(hipIpcGetEventHandle(&h, c->event));
   std::memcpy(handle_out, &h, sizeof(h));
@@ -101,15 +102,16 @@ extern "C" mccsResult_t mccsCommEventHandle(mccsComm_t comm, void* handle_out) {
 extern "C" mccsResult_t mccsCommStream(mccsComm_t comm, hipStream_t* stream) {
   Comm* c = (Comm*)comm;
   if (!c || !stream) return mccsInvalidArgument;
-  *stream = c->stream;
-  return mccsSuccess;
+  return comm_stream(c, stream);
 }
 
 extern "C" mccsResult_t mccsCommWaitEvent(mccsComm_t comm, void* event) {
   Comm* c = (Comm*)comm;
   if (!c || !event) return mccsInvalidArgument;
   DeviceGuard g(c->device);
-  MCCS_HIP(hipStreamWaitEvent(c->stream, (hipEvent_t)event, 0));
+  hipStream_t st = nullptr;
+  MCCS_CHECK(comm_stream(c, &st));
+  MCCS_HIP(hipStreamWaitEvent(st, (hipEvent_t)event, 0));
   return mccsSuccess;
 }
 

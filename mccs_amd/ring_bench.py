@@ -87,16 +87,22 @@ def _subgroup_exchange(dist, group, n):
     return exchange
 
 
-def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, group=None, full=None):
+def _default_modes(C):
+    return [("uncached-fifo", C.CommConfig(timeout_ms=60000)),
+            ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000)),
+            ("sender-side-uncached-fifo", C.CommConfig(locality=C.LOCALITY_SENDER, timeout_ms=60000)),
+            ("sender-side-cached-fifo", C.CommConfig(locality=C.LOCALITY_SENDER, fifo_memory=C.FIFO_DEVICE,
+                                                     timeout_ms=60000))]
+
+
+def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, group=None, full=None, modes=None,
+                         required=True):
     """Build the communicator; check an exact-sum fp32 AllReduce bit for bit
     on every rank (and, with full=(n, torch dtype, AllReduceDataType), one at
-    the timed size and dtype); on failure rebuild with the next FIFO mode."""
-    attempts = [("uncached-fifo", C.CommConfig(timeout_ms=60000)),
-                ("cached-fifo+system-fences", C.CommConfig(fifo_memory=C.FIFO_DEVICE, timeout_ms=60000)),
-                ("sender-side-uncached-fifo", C.CommConfig(locality=C.LOCALITY_SENDER, timeout_ms=60000)),
-                ("sender-side-cached-fifo", C.CommConfig(locality=C.LOCALITY_SENDER, fifo_memory=C.FIFO_DEVICE,
-                                                         timeout_ms=60000))]
-    for name, cfg in attempts:
+    the timed size and dtype); on failure rebuild with the next FIFO mode.
+    Returns (comm, mode name), or (None, None) when no mode passes and not
+    required."""
+    for name, cfg in (modes or _default_modes(C)):
         try:
             comm = C.init_communicator_rank(rank, world, device, exchange, cfg)
         except Exception as e:  # noqa: BLE001  (e.g. IPC refuses this memory kind: try the next mode)
@@ -124,7 +130,48 @@ def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, gro
         if agree(dist, ok, group):
             return comm, name
         comm.destroy()
-    raise SystemExit("ring allreduce failed validation in every FIFO mode")
+    if required:
+        raise SystemExit("ring allreduce failed validation in every FIFO mode")
+    return None, None
+
+
+def _autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for, warmup=2, reps=3):
+    """Transport placement chosen on the node itself: FIFO data at the
+    receiver (remote writes) or at the sender (remote reads, the reference's
+    SHM layout), each at the auto lane count and at 16 lanes per channel.
+    Every candidate is validated exactly like the timed communicator; the
+    fastest (max over ranks) is kept.  MCCS_LOCALITY / MCCS_LANES pin a
+    dimension.  Returns (comm, mode, table)."""
+    locs = [None] if "MCCS_LOCALITY" in os.environ else [C.LOCALITY_RECEIVER, C.LOCALITY_SENDER]
+    lanes_opts = [None] if "MCCS_LANES" in os.environ else [None, 16]
+    best, table, seen = None, [], set()
+    for loc in locs:
+        lname = {None: "env", C.LOCALITY_RECEIVER: "receiver", C.LOCALITY_SENDER: "sender"}[loc]
+        for lanes in lanes_opts:
+            modes = [(f"{lname}-uncached-fifo", C.CommConfig(locality=loc, lanes=lanes, timeout_ms=60000)),
+                     (f"{lname}-cached-fifo+system-fences",
+                      C.CommConfig(locality=loc, lanes=lanes, fifo_memory=C.FIFO_DEVICE, timeout_ms=60000))]
+            comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, full=full,
+                                              modes=modes, required=False)
+            if comm is None:
+                table.append({"mode": f"{lname}/lanes={lanes or 'auto'}", "ok": False})
+                continue
+            key = (mode, comm.lanes)
+            if key in seen:  # auto lanes already == 16
+                comm.destroy()
+                continue
+            seen.add(key)
+            el = max_over_ranks(dist, _time_steps(torch, dist, comm, step_for(comm), warmup, reps))
+            table.append({"mode": mode, "lanes": comm.lanes, "ms_per_step": round(el / reps * 1e3, 4)})
+            if best is None or el < best[0]:
+                if best is not None:
+                    best[1].destroy()
+                best = (el, comm, mode)
+            else:
+                comm.destroy()
+    if best is None:
+        raise SystemExit("ring allreduce failed validation in every transport mode")
+    return best[1], best[2], table
 
 
 def _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev) -> bool:
@@ -224,16 +271,22 @@ def run(args):
     # per-slice wait / stream timing on this rank's GPU (3 atomics per slice
     # per workgroup): reported with the result to show where ring time goes
     os.environ.setdefault("MCCS_RING_PROFILE", "1")
-    comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, full=(n, tdt, code))
-
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     x = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(tdt)
     y = torch.empty_like(x)
     stream = torch.cuda.current_stream()
 
-    def step():
-        C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, stream)
+    def step_for(cm):
+        return lambda: C.all_reduce(cm, x, y, n, code, C.AllReduceOpType.Sum, stream)
+
+    tune_table = None
+    if getattr(args, "no_autotune", False):
+        comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, full=(n, tdt, code))
+    else:
+        comm, mode, tune_table = _autotune(torch, dist, C, rank, world, device, dev, exchange, (n, tdt, code),
+                                           step_for)
+    step = step_for(comm)
 
     K = args.steps
     C.ring_profile(device, reset=True)
@@ -270,6 +323,7 @@ def run(args):
                             f"buckets, chunked FIFO pipeline ({WORKLOADS.get((dt_name, args.size_mib), 'custom')})",
                 "bytes_per_rank": nbytes, "channels": comm.nchannels, "lanes": comm.lanes,
                 "block_threads": comm.block_threads, "rings": rings, "fifo_mode": mode,
+                "transport_autotune": tune_table,
                 "validated_exact_sum_4MiB": True, "validated_exact_sum_full_size_before_timing": True,
                 "validated_exact_sum_full_size_after_timing": full_ok,
                 "busbw_GBps": round(busbw, 3), "parallelism": f"ring{world}",
