@@ -301,6 +301,8 @@ mccsResult_t comm_make_event_ipc(Comm* c) {
 
 mccsResult_t comm_free(Comm* c) {
   DeviceGuard g(c->device);
+  // the last launch (any stream) must be done before its arenas are reused
+  if (c->event) (void)hipEventSynchronize(c->event);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
     if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)hipIpcCloseMemHandle(c->peer_arena[r]);
