@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of reduce variants (stderr)")
     ap.add_argument("--sweep-reg", action="store_true", help="interleaved A/B of the REG loop's map/policy/grid")
+    ap.add_argument("--sweep-cfgs", default=None,
+                    help="interleaved A/B of explicit configs 'v,u,pol,bpc,s,w;...' (stderr)")
+    ap.add_argument("--sweep-rounds", type=int, default=5)
     ap.add_argument("--no-autotune", action="store_true",
                     help="N>1: skip the on-node choice of FIFO placement / lanes (library defaults + fallbacks)")
     ap.add_argument("--no-hot", action="store_true", help="skip the same-buffer measurement (profiling)")
@@ -167,8 +170,10 @@ def bench_reduce(args) -> dict:
             raise SystemExit("bench_reduce: result mismatch vs a+b")
         del ref
 
-    if args.sweep or args.sweep_reg:
-        sweep_variants(sets, n, code, stream, reg_only=args.sweep_reg)
+    if args.sweep or args.sweep_reg or args.sweep_cfgs:
+        # 'v,u,pol,bpc,s,w[,grid]' (grid: LDS grid cap, 0 = default)
+        cfgs = [tuple(int(x) for x in c.split(",")) for c in args.sweep_cfgs.split(";")] if args.sweep_cfgs else None
+        sweep_variants(sets, n, code, stream, reg_only=args.sweep_reg, cfgs=cfgs, rounds=args.sweep_rounds)
 
     for _ in range(args.warmup):
         step()
@@ -261,21 +266,24 @@ def hbm_calibration(sets, n, code, stream) -> dict:
     return {"copy_1to1_GBps": round(2 * nb / t_copy / 1e9, 1)}
 
 
-def sweep_variants(sets, n, code, stream, reg_only=False):
+def sweep_variants(sets, n, code, stream, reg_only=False, cfgs=None, rounds=5):
     """Interleaved rounds of reduce variants in one process, rotating buffer
     sets like the timed loop (stderr)."""
     import torch
 
     import mccs_amd
 
-    cfgs = []
-    if reg_only:  # REG: grid-strided (1) / per-block contiguous (3) tiles / wave rows (4), policy, grid
+    if cfgs:
+        pass
+    elif reg_only:  # REG: grid-strided (1) / per-block contiguous (3) tiles / wave rows (4), policy, grid
+        cfgs = []
         for v in (1, 3, 4):
             for u in (2, 4, 8):
                 for pol in (1, 2, 3):
                     for bpc in (8, 16, 32):
                         cfgs.append((v, u, pol, bpc, 0, 0))
     else:
+        cfgs = []
         for u, bpc in ((4, 32), (4, 16), (8, 16)):  # REG
             cfgs.append((1, u, 1, bpc, 0, 0))
         for u, s, w in ((1, 3, 4), (2, 2, 4), (2, 3, 4), (4, 2, 4), (4, 3, 4), (4, 4, 4), (8, 2, 4),
@@ -284,14 +292,17 @@ def sweep_variants(sets, n, code, stream, reg_only=False):
                 if w * s * 2 * u * bpc <= 160:
                     cfgs.append((2, u, 1, bpc, s, w))
         cfgs.append((2, 4, 2, 1, 3, 4))  # plain LDS-DMA reads
+        for pol in (3, 4, 5):  # write-through stores: nt+sc1, sc1, sc0+sc1+nt
+            cfgs.append((2, 4, pol, 1, 3, 4))
         cfgs.append((1, 4, 0, 8, 0, 0))
     c0 = sets[0][2]
     alg = 3 * c0.numel() * c0.element_size()
     times = {cfg: [] for cfg in cfgs}
     k = 0
-    for _ in range(5):
+    for _ in range(rounds):
         for cfg in cfgs:
-            mccs_amd.tune(*cfg)
+            mccs_amd.tune(*cfg[:6])
+            mccs_amd.tune_grid(cfg[6] if len(cfg) > 6 else 0)
             for _ in range(2):
                 a_, b_, c_ = sets[k % len(sets)]
                 k += 1
@@ -308,9 +319,10 @@ def sweep_variants(sets, n, code, stream, reg_only=False):
     rows = sorted(((sorted(v)[len(v) // 2], min(v), cfg) for cfg, v in times.items()))
     for med, mn, cfg in rows:
         print(f"[sweep] variant={cfg[0]} unroll={cfg[1]} policy={cfg[2]} bpc={cfg[3]} stages={cfg[4]} "
-              f"waves={cfg[5]} median {med*1e3:.2f} us  {alg/med/1e6:.1f} GB/s  (best {alg/mn/1e6:.1f})",
+              f"waves={cfg[5]} grid={cfg[6] if len(cfg) > 6 else 0} median {med*1e3:.2f} us  {alg/med/1e6:.1f} GB/s  (best {alg/mn/1e6:.1f})",
               file=sys.stderr)
     mccs_amd.tune()
+    mccs_amd.tune_grid(0)
 
 
 def relaunch_under_torchrun(args) -> int:

@@ -58,7 +58,8 @@ mccsResult_t mccs_hip_reduce_copy(void *const *dsts, int ndsts, const void *cons
 /* Select the main loop (0 = default), unroll = KiB per source per wave tile
  * for LDS / 16-byte packs per lane for REG (1/2/4/8, 0 = default), cache
  * policy (0 plain, 1 non-temporal, -1 default; REG: 2 nt loads + plain
- * stores, 3 plain loads + nt stores; LDS: 2 plain LDS-DMA + nt stores),
+ * stores, 3 plain loads + nt stores; LDS: 2 plain LDS-DMA + nt stores,
+ * 3 nt + sc1 stores, 4 write-through sc1 stores (default), 5 sc0 sc1 nt),
  * persistent blocks per CU,
  * LDS ring stages (2..4) and waves per block (4/8); 0 = default for each.
  * Process-wide; for benchmarking and tests. */
@@ -66,6 +67,9 @@ mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int block
                                   int waves);
 void mccs_hip_reduce_get_tune(int *variant, int *unroll, int *policy, int *blocks_per_cu, int *stages,
                               int *waves);
+/* Caps the LDS main loop's grid at `blocks` workgroups (0 = blocks_per_cu x
+ * CUs, the default).  Process-wide; for benchmarking. */
+mccsResult_t mccs_hip_reduce_tune_grid(int blocks);
 
 /* ======================================================================
  * Ring collectives: device kernels (reference src/collectives) and the

@@ -7,6 +7,6 @@ Layers:
   mccs_amd/*.py            ctypes face mirroring libmccs (src/libmccs)
 """
 from ._lib import DataType, MccsError, RedOp, load  # noqa: F401
-from .reduce import get_tune, reduce, reduce_copy, tune  # noqa: F401
+from .reduce import get_tune, reduce, reduce_copy, tune, tune_grid  # noqa: F401
 
 __version__ = "0.1.0"

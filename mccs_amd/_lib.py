@@ -83,6 +83,7 @@ SIGNATURES: dict[str, tuple] = {
     ),
     "mccs_hip_reduce_tune": (_c_int, [_c_int] * 6),
     "mccs_hip_reduce_get_tune": (None, [_P(_c_int)] * 6),
+    "mccs_hip_reduce_tune_grid": (_c_int, [_c_int]),
     # ring kernels + communicator runtime
     "mccs_hip_coll_kernel": (_c_void_p, [_c_int, _c_int, _c_int]),
     "mccs_hip_launch_coll": (

@@ -260,16 +260,20 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
 // non-temporal DMA reads and stores, 4 KiB per source per wave tile, a
 // 3-stage ring (double buffering plus one tile of slack), 4 waves, one block
 // per CU: 6.52 TB/s against 6.43 for the best REG loop on the same box.
-// Without nt on the DMA reads the same loop streams 5.9 TB/s; see DESIGN.md.
+// Without nt on the DMA reads the same loop streams 5.9 TB/s.  Stores are
+// write-through (sc1), so no dirty lines wait in the XCD L2s for the
+// end-of-kernel writeback: +0.4 % over nt stores in 30-round A/Bs; see
+// DESIGN.md.
 struct ReduceTune {
   int variant = MCCS_REDUCE_VARIANT_LDS;
   int unroll = 4;  // LDS: 4 KiB per source per wave tile
-  int policy = 1;  // 1 = non-temporal LDS-DMA reads + nt stores
+  int policy = 4;  // nt LDS-DMA reads + write-through (sc1) stores; 1 = nt stores
   int blocks_per_cu = 1;  // LDS: one 4-wave block per CU (96 KiB of LDS ring)
   int stages = 3;
   int waves = 4;
 };
 static ReduceTune g_tune;
+static int g_grid_cap = 0;  // mccs_hip_reduce_tune_grid
 static int g_num_cus = 0;
 
 static int num_cus() {
@@ -333,7 +337,9 @@ template <int DT, int OP, int U, int S, int W>
 static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t st) {
   static_assert(lds_fits<U, S, W>(), "LDS budget");
   const size_t lds = (size_t)W * S * 2 * U * 1024;
-  // pol: 0 plain DMA + plain stores, 1 nt DMA + nt stores, 2 plain DMA + nt stores
+  // pol: 0 plain DMA + plain stores, 1 nt DMA + nt stores, 2 plain DMA + nt
+  // stores; nt DMA with write-through stores (tuning grid only): 3 nt+sc1,
+  // 4 sc1, 5 sc0+sc1+nt
   auto kn = reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNonTemporal>;
   auto kp = reduce_lds_kernel<DT, OP, U, S, W, kPlain, kPlain>;
   auto ks = reduce_lds_kernel<DT, OP, U, S, W, kPlain, kNonTemporal>;
@@ -344,13 +350,29 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
     (void)hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set.store(true, std::memory_order_relaxed);
   }
+  if constexpr (tuned_grid<DT, OP>() && U == 4 && S == 3 && W == 4) {
+    if (pol >= 3) {
+      auto kw = pol == 3 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNtWriteThrough>
+                : pol == 4 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kWriteThrough>
+                           : reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kSystemNt>;
+      (void)hipFuncSetAttribute((const void*)kw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      constexpr int PACK = kPackElems<DT>;
+      const int64_t npack = a.count / PACK;
+      const int64_t wtiles = (npack + 64 * U - 1) / (64 * U);
+      int64_t blocks = (wtiles + W - 1) / W;
+      const int64_t gmax = g_grid_cap > 0 ? g_grid_cap : (int64_t)num_cus() * bpc;
+      const int grid = (int)(blocks < gmax ? (blocks > 0 ? blocks : 1) : gmax);
+      hipLaunchKernelGGL(kw, dim3(grid), dim3(W * 64), lds, st, a);
+      return hipGetLastError();
+    }
+  }
   constexpr int PACK = kPackElems<DT>;
   const int64_t npack = a.count / PACK;
   const int64_t wtiles = (npack + 64 * U - 1) / (64 * U);
   int64_t blocks = (wtiles + W - 1) / W;
-  const int64_t gmax = (int64_t)num_cus() * bpc;
+  const int64_t gmax = g_grid_cap > 0 ? g_grid_cap : (int64_t)num_cus() * bpc;
   const int grid = (int)(blocks < gmax ? (blocks > 0 ? blocks : 1) : gmax);
-  if (pol == 1)
+  if (pol == 1 || pol >= 3)
     hipLaunchKernelGGL(kn, dim3(grid), dim3(W * 64), lds, st, a);
   else if (pol == 2)
     hipLaunchKernelGGL(ks, dim3(grid), dim3(W * 64), lds, st, a);
@@ -469,7 +491,7 @@ extern "C" mccsResult_t mccs_hip_reduce(void* dst, const void* const* srcs, int 
 extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu,
                                              int stages, int waves) {
   if (variant < 0 || variant > MCCS_REDUCE_VARIANT_REG_ROWS) return mccsInvalidArgument;
-  if (policy > 3) return mccsInvalidArgument;
+  if (policy > 5) return mccsInvalidArgument;
   if (unroll < 0 || unroll > 8 || (unroll & (unroll - 1))) return mccsInvalidArgument;
   if (stages < 0 || stages == 1 || stages > 4 || waves < 0 || (waves != 0 && (waves < 4 || waves > 8 || waves == 7)))
     return mccsInvalidArgument;
@@ -478,7 +500,7 @@ extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy
   t.variant = variant ? variant : d.variant;
   const bool reg = t.variant != MCCS_REDUCE_VARIANT_LDS;
   t.unroll = unroll ? unroll : 4;
-  t.policy = policy < 0 ? d.policy : (reg ? policy : (policy == 3 ? 1 : policy));
+  t.policy = policy < 0 ? (reg ? 1 : d.policy) : (reg ? (policy > 3 ? 1 : policy) : policy);
   t.blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : (reg ? 32 : 1);
   t.stages = stages ? stages : d.stages;
   t.waves = waves ? waves : d.waves;
@@ -495,4 +517,10 @@ extern "C" void mccs_hip_reduce_get_tune(int* variant, int* unroll, int* policy,
   if (blocks_per_cu) *blocks_per_cu = g_tune.blocks_per_cu;
   if (stages) *stages = g_tune.stages;
   if (waves) *waves = g_tune.waves;
+}
+
+extern "C" mccsResult_t mccs_hip_reduce_tune_grid(int blocks) {
+  if (blocks < 0) return mccsInvalidArgument;
+  g_grid_cap = blocks;
+  return mccsSuccess;
 }

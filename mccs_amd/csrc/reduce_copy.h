@@ -11,8 +11,10 @@
 
 namespace mccs {
 
-// Cache policy for a stream of 16-byte accesses.
-enum Policy : int { kPlain = 0, kNonTemporal = 1 };
+// Cache policy for a stream of 16-byte accesses.  The write-through forms
+// (sc1: the store goes through this XCD's L2 to memory instead of staying
+// dirty there until the end-of-kernel writeback) are store-only.
+enum Policy : int { kPlain = 0, kNonTemporal = 1, kNtWriteThrough = 2, kWriteThrough = 3, kSystemNt = 4 };
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
@@ -22,6 +24,12 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
 template <int POL>
 __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
   if constexpr (POL == kNonTemporal) __builtin_nontemporal_store(v, p);
+  else if constexpr (POL == kNtWriteThrough)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == kWriteThrough)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == kSystemNt)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
   else *p = v;
 }
 

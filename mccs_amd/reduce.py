@@ -74,6 +74,11 @@ def tune(variant: int = 0, unroll: int = 0, policy: int = -1, blocks_per_cu: int
                "mccs_hip_reduce_tune")
 
 
+def tune_grid(blocks: int = 0) -> None:
+    """Caps the LDS main loop's grid (0 = default: blocks_per_cu x CUs)."""
+    _lib.check(_lib.load().mccs_hip_reduce_tune_grid(int(blocks)), "mccs_hip_reduce_tune_grid")
+
+
 def get_tune() -> dict:
     import ctypes
 

@@ -139,7 +139,8 @@ def test_invalid_arguments_fail_loudly():
     (2, 4, 1, 2, 2, 4), (2, 1, 1, 1, 3, 4), (2, 2, 1, 2, 2, 8), (2, 4, 1, 1, 4, 4), (2, 8, 1, 1, 2, 4),
     (2, 4, 2, 1, 3, 5), (2, 4, 1, 1, 3, 6), (2, 2, 2, 2, 3, 6), (2, 4, 0, 1, 2, 6), (2, 1, 2, 1, 2, 8),
     (1, 4, 2, 16, 0, 0), (1, 8, 3, 32, 0, 0), (3, 4, 1, 16, 0, 0), (3, 2, 2, 32, 0, 0), (3, 8, 3, 8, 0, 0),
-    (4, 4, 1, 32, 0, 0), (4, 8, 1, 16, 0, 0), (4, 2, 0, 8, 0, 0)])
+    (4, 4, 1, 32, 0, 0), (4, 8, 1, 16, 0, 0), (4, 2, 0, 8, 0, 0), (2, 4, 3, 1, 3, 4), (2, 4, 4, 1, 3, 4),
+    (2, 4, 5, 1, 3, 4)])
 @pytest.mark.parametrize("code", [6, 7, 9])
 def test_reduce_variants(orc, variant, unroll, policy, bpc, stages, waves, code):
     import mccs_amd
