@@ -11,7 +11,7 @@ import enum
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmccs_hip.so")
+LIB_PATH = os.environ.get("MCCS_LIB_PATH") or os.path.join(_HERE, "libmccs_hip.so")  # override: A/B builds
 
 
 class DataType(enum.IntEnum):

@@ -43,7 +43,8 @@ __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
 // iteration are issued before the first use; the partial last iteration is a
 // single predicated pass.  Every pointer must be 16-byte aligned when
 // ALIGNED; otherwise a typed element loop runs (reference ReduceCopyMulti).
-template <int DT, int OP, int U, int NS, int ND, int NTMASK>
+// DP0 / DP1: store policy of destination 0 / 1.
+template <int DT, int OP, int U, int NS, int ND, int NTMASK, int DP0 = kPlain, int DP1 = kPlain>
 __device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1, void* d0, void* d1, int64_t nelem,
                                                  int tid, int nthr) {
   static_assert(NS >= 1 && NS <= 2 && ND >= 1 && ND <= 2, "ring primitives move 1-2 sources to 1-2 destinations");
@@ -80,10 +81,10 @@ __device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1,
         for (int u = 0; u < U; ++u) v[u] = pack_op<DT, OP>(v[u], w[u]);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) st16<kPlain>(x + q + 64u * u, v[u]);
+      for (int u = 0; u < U; ++u) st16<DP0>(x + q + 64u * u, v[u]);
       if constexpr (ND > 1) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) st16<kPlain>(y + q + 64u * u, v[u]);
+        for (int u = 0; u < U; ++u) st16<DP1>(y + q + 64u * u, v[u]);
       }
     }
     if (base < npack) {  // partial iteration: same layout, predicated
@@ -104,8 +105,8 @@ __device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1,
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (q + 64u * u < npack) {
-          st16<kPlain>(x + q + 64u * u, v[u]);
-          if constexpr (ND > 1) st16<kPlain>(y + q + 64u * u, v[u]);
+          st16<DP0>(x + q + 64u * u, v[u]);
+          if constexpr (ND > 1) st16<DP1>(y + q + 64u * u, v[u]);
         }
     }
     done = (int64_t)npack * PACK;
