@@ -41,10 +41,17 @@ def main():
         dist.all_gather_object(out, b)
         return out
 
+    # FIFO memory kind x data placement (receiver-side: remote writes;
+    # sender-side: remote reads, the reference SHM layout)
+    all_modes = {"uncached": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER), "device": (C.FIFO_DEVICE, C.LOCALITY_RECEIVER),
+                 "sender-uncached": (C.FIFO_UNCACHED, C.LOCALITY_SENDER),
+                 "sender-device": (C.FIFO_DEVICE, C.LOCALITY_SENDER)}
+    names = os.environ.get("IPC_MODES", "uncached,device").split(",")
     results = {}
-    for mode, fifo in (("uncached", C.FIFO_UNCACHED), ("device", C.FIFO_DEVICE)):
+    for mode in names:
+        fifo, loc = all_modes[mode]
         comm = C.init_communicator_rank(rank, world, dev, exchange,
-                                        C.CommConfig(fifo_memory=fifo, timeout_ms=20000))
+                                        C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000))
         for code, count in ((2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)):
             rng = np.random.default_rng(count * 31 + rank)
             x = vnode.gen(code, count, rng)

@@ -1,9 +1,10 @@
 """GPU: ring AllReduce across processes through IPC-mapped FIFO arenas.
 
-Two ranks in two processes (tests/ipc_worker.py under torch.distributed.run),
-both on cuda:0 of the one-GPU box: exercises hipIpcGetMemHandle /
-hipIpcOpenMemHandle, the two-phase connect and cross-process flag hand-offs
-in both FIFO memory modes, bit for bit against the oracle.
+Two and four ranks in as many processes (tests/ipc_worker.py under
+torch.distributed.run), all on cuda:0 of the one-GPU box: exercises
+hipIpcGetMemHandle / hipIpcOpenMemHandle, the two-phase connect and
+cross-process flag hand-offs in both FIFO memory kinds and both data
+placements, bit for bit against the oracle.
 """
 import json
 import os
@@ -23,12 +24,15 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def test_two_process_ring_matches_oracle():
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+@pytest.mark.parametrize("world,modes", [(2, "uncached,device,sender-uncached,sender-device"),
+                                         (4, "uncached,sender-uncached")])
+def test_multi_process_ring_matches_oracle(world, modes):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(HERE, "ipc_worker.py")]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", IPC_MODES=modes)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=os.path.dirname(HERE))
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(lines[-1])
     assert res["all_ok"], res
+    assert res["world"] == world
