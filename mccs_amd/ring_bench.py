@@ -286,15 +286,31 @@ def run(args):
     else:
         comm, mode, tune_table = _autotune(torch, dist, C, rank, world, device, dev, exchange, (n, tdt, code),
                                            step_for)
-    step = step_for(comm)
-
     K = args.steps
-    C.ring_profile(device, reset=True)
-    elapsed = max_over_ranks(dist, _time_steps(torch, dist, comm, step, args.warmup, K))
-    prof = C.ring_profile(device, reset=True)
-    per_step = elapsed / K
+    failed_after_timing = []
+    while True:
+        step = step_for(comm)
+        C.ring_profile(device, reset=True)
+        elapsed = max_over_ranks(dist, _time_steps(torch, dist, comm, step, args.warmup, K))
+        prof = C.ring_profile(device, reset=True)
+        per_step = elapsed / K
+        full_ok = _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev)
+        if os.environ.get("MCCS_BENCH_INJECT_MISMATCH") == "1" and not failed_after_timing:
+            full_ok = False  # fault injection: exercises the re-timing path below
+        full_ok = agree(dist, full_ok)
+        if full_ok or failed_after_timing:
+            break
+        # the timed mode passed validation but a later sum was wrong: re-time
+        # with the most conservative hand-off (release/acquire fences on cached
+        # FIFOs), or with uncached FIFOs if that was the failing mode
+        failed_after_timing.append(mode)
+        print(f"[rank {rank}] {mode}: full-size exact-sum mismatch after timing; re-timing", flush=True)
+        comm.destroy()
+        cached = "uncached" not in mode
+        fallback = [m for m in _default_modes(C) if ("uncached" in m[0]) == bool(cached)]
+        comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, full=(n, tdt, code),
+                                          modes=fallback)
     del x, y
-    full_ok = agree(dist, _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev))
     algbw = nbytes / per_step / 1e9
     busbw = algbw * 2 * (world - 1) / world
     link_bytes = 2 * (world - 1) / world * nbytes
@@ -326,6 +342,7 @@ def run(args):
                 "transport_autotune": tune_table,
                 "validated_exact_sum_4MiB": True, "validated_exact_sum_full_size_before_timing": True,
                 "validated_exact_sum_full_size_after_timing": full_ok,
+                "failed_after_timing": failed_after_timing,
                 "busbw_GBps": round(busbw, 3), "parallelism": f"ring{world}",
                 "rank0_slice_profile": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()},
                 # ranks sharing one GPU (a 1-GPU box): FIFO hand-offs stay in HBM, no xGMI link
