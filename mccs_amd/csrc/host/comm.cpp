@@ -93,8 +93,7 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
   k.slice_steps = ALLREDUCE_CHUNKSTEPS;
   if (const char* v = std::getenv("MCCS_SLICE_STEPS")) k.slice_steps = std::atoi(v) == 2 ? 2 : 4;
   if (const char* v = std::getenv("MCCS_RING_PROFILE")) k.profile = std::atoi(v) != 0;
-  DeviceGuard g(c->device);
-  MCCS_HIP(ring_set_device_cfg(k));
+  c->kcfg = k;  // travels in every launch's arguments (no device global)
   return mccsSuccess;
 }
 

@@ -135,6 +135,7 @@ struct Comm {
   hipEvent_t user_event = nullptr;  // user -> comm
   bool connected = false;
   bool failed = false;
+  mccsRingKernelCfg kcfg{};  // hand-off policy of this comm's launches (launch arguments)
   // plan state
   std::vector<ChannelSchedule> sched;
   int plan_func = -1, plan_dtype = -1, plan_op = -1, plan_threads = 0;
@@ -157,7 +158,6 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
 const void* ring_kernel_ptr(int func, int dtype, int op);
 const void* ring_multi_kernel_ptr(int func, int dtype, int op);
 int coresident_ring_blocks(int block, int device);
-hipError_t ring_set_device_cfg(const mccsRingKernelCfg& cfg);
 hipError_t ring_take_device_error(unsigned* err);
 hipError_t ring_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_flush_caches(hipStream_t st);

@@ -271,25 +271,29 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     }
     const unsigned grid = (unsigned)(lds[0].nch_used * c0->lanes);
     const unsigned block = (unsigned)c0->block_threads;
-    if (idx.size() == 1) {
-      mccsDevComm* dcomm = (mccsDevComm*)c0->d_comm;
-      void* args[3] = {&dcomm, &lds[0].mask, &lds[0].work};
-      MCCS_HIP(hipLaunchKernel(lds[0].fn, dim3(grid), dim3(block), args, 0, st));
-    } else {
-      if (idx.size() > MCCS_MULTI_MAX_RANKS) return mccsInvalidUsage;
-      mccsMultiLaunchArgs ma;
-      std::memset(&ma, 0, sizeof(ma));
-      ma.channelMask = lds[0].mask;
-      for (size_t k = 0; k < idx.size(); ++k) {
-        if (lds[k].mask != lds[0].mask || lds[k].multi_fn != lds[0].multi_fn ||
-            comms[idx[k]]->lanes != c0->lanes || comms[idx[k]]->block_threads != c0->block_threads)
-          return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
-        ma.comm[k] = (mccsDevComm*)comms[idx[k]]->d_comm;
-        ma.work[k] = lds[k].work;
-      }
-      void* args[1] = {&ma};
-      MCCS_HIP(hipLaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, 0, st));
+    // Communicator launches carry their hand-off policy in the arguments
+    // (one launch per device; blockIdx.y = rank slot when ranks share it).
+    // Fused ranks take the safest policy of the group.
+    if (idx.size() > MCCS_MULTI_MAX_RANKS) return mccsInvalidUsage;
+    mccsMultiLaunchArgs ma;
+    std::memset(&ma, 0, sizeof(ma));
+    ma.channelMask = lds[0].mask;
+    ma.cfg = c0->kcfg;
+    for (size_t k = 0; k < idx.size(); ++k) {
+      const Comm* ck = comms[idx[k]];
+      if (lds[k].mask != lds[0].mask || lds[k].multi_fn != lds[0].multi_fn || ck->lanes != c0->lanes ||
+          ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps)
+        return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
+      ma.comm[k] = (mccsDevComm*)ck->d_comm;
+      ma.work[k] = lds[k].work;
+      if (ck->kcfg.fence_mode != MCCS_FENCE_UNCACHED) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
+      ma.cfg.timeout_ticks = (ma.cfg.timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)
+                                 ? 0
+                                 : std::max(ma.cfg.timeout_ticks, ck->kcfg.timeout_ticks);
+      ma.cfg.profile |= ck->kcfg.profile;
     }
+    void* args[1] = {&ma};
+    MCCS_HIP(hipLaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, 0, st));
     MCCS_HIP(hipEventRecord(c0->event, st));
     if (events) {
       for (size_t k = 0; k < idx.size(); ++k) {

@@ -20,7 +20,10 @@
 // per source fits without spilling, which a 1024-thread bound (128 VGPRs) did not.
 #define MCCS_RING_MAX_THREADS 576
 
-// Fence policy for FIFO hand-offs (device global, per device; set by the host).
+// Fence policy for FIFO hand-offs.  Communicator launches carry it in their
+// launch arguments (mccsMultiLaunchArgs.cfg); the reference-named kernels,
+// launched by an external planner that cannot say what memory its FIFOs are,
+// always run with the reference defaults (system-scope fences, 2-step slices).
 #define MCCS_FENCE_SYSTEM 0   // FIFO memory may be cached: system-scope release/acquire
 #define MCCS_FENCE_UNCACHED 1 // FIFO memory is uncached (hipDeviceMallocUncached): drains only
 
@@ -43,11 +46,13 @@ struct mccsRingKernelCfg {
 #define MCCS_PROF_WORK 2    // flags satisfied -> stores drained, both barriers included
 #define MCCS_PROF_N 4
 
-// Multi-rank launch (several communicators of one device in ONE launch, used
-// when ranks share a GPU: tests' virtual node).  blockIdx.y = rank slot.
+// Communicator launch: one or several communicators of one device in ONE
+// launch (several when ranks share a GPU: tests' virtual node).
+// blockIdx.y = rank slot.
 #define MCCS_MULTI_MAX_RANKS 16
 struct mccsMultiLaunchArgs {
   struct mccsDevComm* comm[MCCS_MULTI_MAX_RANKS];
   struct mccsDevWork* work[MCCS_MULTI_MAX_RANKS];
   uint64_t channelMask;
+  struct mccsRingKernelCfg cfg;  // this launch's hand-off policy
 };
