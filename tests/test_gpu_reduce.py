@@ -179,3 +179,41 @@ def test_reduce_full_benchmark_size(orc):
         orc.reduce_mt(7, 0, [ha, hb], ref, 8)
         assert np.array_equal(c.cpu().numpy().view(np.uint32), ref.view(np.uint32)), variant
     mccs_amd.tune()
+
+
+def test_reduce_captured_in_hip_graph(orc):
+    """The chunk reduce is a plain stream-ordered launch, so a caller can
+    capture a bucket of reduces into a hipGraph and replay it (one graph
+    launch instead of one host launch per bucket)."""
+    import mccs_amd
+    import torch
+
+    rng = np.random.default_rng(11)
+    n = (1 << 20) + 5
+    hs = [[rand(7, n, rng) for _ in range(2)] for _ in range(3)]
+    srcs = [[torch.from_numpy(h).cuda() for h in pair] for pair in hs]
+    outs = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(3)]
+    mccs_amd.reduce(outs[0], srcs[0])  # first call outside capture (one-time attribute setup)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for k in range(3):
+                mccs_amd.reduce(outs[k], srcs[k], stream=s)
+    for o in outs:
+        o.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    for k in range(3):
+        (ref,) = orc.reduce_copy(7, 0, hs[k])
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), ref.view(np.uint32)), k
+    # new inputs in the same buffers: the replay reads them
+    for k in range(3):
+        srcs[k][0].mul_(2)
+    g.replay()
+    torch.cuda.synchronize()
+    for k in range(3):
+        (ref,) = orc.reduce_copy(7, 0, [srcs[k][0].cpu().numpy(), hs[k][1]])
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), ref.view(np.uint32)), k
