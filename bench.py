@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--sweep-rounds", type=int, default=5)
     ap.add_argument("--no-autotune", action="store_true",
                     help="N>1: skip the on-node choice of FIFO placement / lanes (library defaults + fallbacks)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="N>1: skip the extra BASELINE configs[3] line (fp16 1 GiB) reported in config")
     ap.add_argument("--no-hot", action="store_true", help="skip the same-buffer measurement (profiling)")
     return ap.parse_args()
 

@@ -355,7 +355,12 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
       auto kw = pol == 3 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNtWriteThrough>
                 : pol == 4 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kWriteThrough>
                            : reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kSystemNt>;
-      (void)hipFuncSetAttribute((const void*)kw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      static std::atomic<unsigned> wt_attr_set{0};  // bit per policy 3..5
+      const unsigned bit = 1u << (pol - 3);
+      if (!(wt_attr_set.load(std::memory_order_relaxed) & bit)) {
+        (void)hipFuncSetAttribute((const void*)kw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        wt_attr_set.fetch_or(bit, std::memory_order_relaxed);
+      }
       constexpr int PACK = kPackElems<DT>;
       const int64_t npack = a.count / PACK;
       const int64_t wtiles = (npack + 64 * U - 1) / (64 * U);

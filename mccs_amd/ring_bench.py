@@ -195,6 +195,30 @@ def _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev) -> bool:
     return ok
 
 
+def _extra_fp16_1gib(torch, dist, C, comm, rank, world, dev, warmup=3, K=10):
+    """BASELINE configs[3] on the communicator just measured: fp16 AllReduce
+    of a 1 GiB bucket per rank, exact-sum validated at full size, algbw."""
+    n = (1 << 30) // 2
+    g = torch.Generator(device=dev)
+    g.manual_seed(3000 + rank)
+    x = (torch.rand(n, device=dev, generator=g) * 2 - 1).to(torch.float16)
+    y = torch.empty_like(x)
+    code = C.AllReduceDataType.Float16
+
+    def step():
+        C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum)
+
+    el = max_over_ranks(dist, _time_steps(torch, dist, comm, step, warmup, K))
+    del x, y
+    torch.cuda.empty_cache()
+    ok = agree(dist, _full_size_exact(torch, C, comm, rank, world, n, torch.float16, code, dev))
+    per = el / K
+    return {"workload": f"{world}x ring allreduce, 1 GiB float16 buckets (BASELINE configs[3])",
+            "ms_per_step": round(per * 1e3, 4), "algbw_GBps": round((1 << 30) / per / 1e9, 3),
+            "busbw_GBps": round((1 << 30) / per / 1e9 * 2 * (world - 1) / world, 3), "steps": K,
+            "validated_exact_sum_full_size": ok}
+
+
 def _out_links(rings, rank):
     """Distinct xGMI links this rank sends on (one per distinct ring successor)."""
     nxt = set()
@@ -311,6 +335,9 @@ def run(args):
         comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, full=(n, tdt, code),
                                           modes=fallback)
     del x, y
+    extra = None
+    if not getattr(args, "no_extra", False) and (dt_name, args.size_mib) == ("float32", 128):
+        extra = _extra_fp16_1gib(torch, dist, C, comm, rank, world, dev)
     algbw = nbytes / per_step / 1e9
     busbw = algbw * 2 * (world - 1) / world
     link_bytes = 2 * (world - 1) / world * nbytes
@@ -362,6 +389,8 @@ def run(args):
             },
             "cpu_baseline": None,
         }
+        if extra is not None:
+            out["config"]["configs3_fp16_1GiB"] = extra
         if not getattr(args, "no_cpu_baseline", False):
             out["cpu_ring_baseline"] = cpu_ring_baseline(C, world)
     comm.destroy()
