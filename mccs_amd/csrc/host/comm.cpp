@@ -205,6 +205,11 @@ mccsResult_t comm_alloc_local(Comm* c) {
   MCCS_HIP(hipHostMalloc((void**)&c->h_work, sizeof(mccsDevWork) * c->work_depth, hipHostMallocMapped));
   MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_work, c->h_work, 0));
   std::memset(c->h_work, 0, sizeof(mccsDevWork) * c->work_depth);
+  MCCS_HIP(hipHostMalloc((void**)&c->h_graph_work, sizeof(mccsDevWork) * Comm::kGraphWorkEntries,
+                         hipHostMallocMapped));
+  MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_graph_work, c->h_graph_work, 0));
+  std::memset(c->h_graph_work, 0, sizeof(mccsDevWork) * Comm::kGraphWorkEntries);
+  c->graph_work_used = 0;
   MCCS_HIP(hipHostMalloc((void**)&c->h_done, sizeof(uint32_t) * MCCS_MAX_NCHANNELS, hipHostMallocMapped));
   MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_done, c->h_done, 0));
   std::memset(c->h_done, 0, sizeof(uint32_t) * MCCS_MAX_NCHANNELS);
@@ -311,6 +316,7 @@ mccsResult_t comm_free(Comm* c) {
   if (c->d_comm) (void)hipFree(c->d_comm);
   if (c->d_abort) (void)hipFree(c->d_abort);
   if (c->h_work) (void)hipHostFree(c->h_work);
+  if (c->h_graph_work) (void)hipHostFree(c->h_graph_work);
   if (c->h_done) (void)hipHostFree(c->h_done);
   if (c->event) (void)hipEventDestroy(c->event);
   if (c->user_event) (void)hipEventDestroy(c->user_event);

@@ -121,6 +121,15 @@ struct Comm {
   uint32_t* h_done = nullptr;
   uint32_t* d_done = nullptr;
   uint32_t work_depth = 4096;
+  // Work lists of launches captured into HIP graphs: a graph replays the
+  // same kernel arguments forever, so its works cannot live in the rolling
+  // FIFO (slots get reused).  Captured launches take entries from this
+  // host-mapped arena for the comm's lifetime (allocated at init: allocation
+  // is not allowed while a stream captures).
+  static constexpr uint32_t kGraphWorkEntries = 2048;
+  mccsDevWork* h_graph_work = nullptr;
+  mccsDevWork* d_graph_work = nullptr;
+  uint32_t graph_work_used = 0;
   uint32_t work_next = 0;      // work_queue_next_available
   uint32_t work_acked_min = 0; // work_queue_acked_min
   std::vector<uint32_t> chan_next;  // per channel work_queue_next_available

@@ -148,6 +148,50 @@ struct LaunchDesc {
   mccsDevWork* work = nullptr;
 };
 
+// A launch being captured into a HIP graph: its works go to the comm's
+// graph arena, laid out like one FIFO upload (first work of channel i at
+// entry i, later ones chained by workNext relative to the head), with
+// inFifo = 0 so replays never write workFifoDone (common.h:153-155).
+static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld) {
+  std::vector<int> chan_list;
+  uint64_t mask = 0;
+  uint32_t work_count = 0;
+  for (int ch = 0; ch < c->nch; ++ch)
+    if (!c->sched[ch].works.empty()) {
+      chan_list.push_back(ch);
+      mask |= 1ull << ch;
+      work_count += (uint32_t)c->sched[ch].works.size();
+    }
+  if (chan_list.empty()) return mccsInternalError;
+  if (c->graph_work_used + work_count > Comm::kGraphWorkEntries) {
+    MCCS_LOG("graph work arena exhausted (%u of %u entries used)", c->graph_work_used, Comm::kGraphWorkEntries);
+    return mccsInvalidUsage;
+  }
+  mccsDevWork* head = c->h_graph_work + c->graph_work_used;
+  const uint32_t nchan = (uint32_t)chan_list.size();
+  uint32_t subsequent = nchan;
+  for (uint32_t nth = 0; nth < nchan; ++nth) {
+    auto& works = c->sched[chan_list[nth]].works;
+    for (size_t wid = 0; wid < works.size(); ++wid) {
+      const bool last = wid == works.size() - 1;
+      const uint32_t next = wid == 0 ? subsequent : subsequent + 1;
+      mccsDevWork dw = to_dev_work(works[wid], false, last, last ? 0u : next);
+      const uint32_t cur = wid == 0 ? nth : subsequent++;
+      head[cur] = dw;
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  ld->mask = mask;
+  ld->nch_used = (int)nchan;
+  ld->work = c->d_graph_work + c->graph_work_used;
+  c->graph_work_used += work_count;
+  ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
+  ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
+  for (auto& s : c->sched) s = ChannelSchedule{};
+  c->plan_pending = false;
+  return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
+}
+
 static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
   std::vector<int> chan_list;
   uint64_t mask = 0;
@@ -253,8 +297,14 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
         return mccsInvalidUsage;  // would deadlock: every block spins on a peer's flag
       }
     }
+    // A capturing stream records this launch into a HIP graph: its work
+    // list must outlive the FIFO's rolling slots (upload_work_graph).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    MCCS_HIP(hipStreamIsCapturing(user_streams[idx[0]], &cap));
+    const bool capturing = cap == hipStreamCaptureStatusActive;
     std::vector<LaunchDesc> lds(idx.size());
-    for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work(comms[idx[k]], &lds[k]));
+    for (size_t k = 0; k < idx.size(); ++k)
+      MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k]) : upload_work(comms[idx[k]], &lds[k]));
     Comm* c0 = comms[idx[0]];
     const bool bridge = c0->cfg.bridge_streams >= 0;
     hipStream_t st = user_streams[idx[0]];

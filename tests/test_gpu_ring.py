@@ -338,3 +338,50 @@ def test_ring_profile_counters(monkeypatch):
         vnode.destroy(comms)
         monkeypatch.delenv("MCCS_RING_PROFILE")
         C.init_all([0])[0].destroy()  # disarm
+
+
+@pytest.mark.parametrize("n,count", [(2, 1 << 20), (4, 300007)])
+def test_allreduce_captured_in_hip_graph(orc, n, count):
+    """AllReduces captured into a HIP graph (torch.cuda.graph) replay with the
+    inputs of each replay, interleaved with eager calls on the same comms:
+    captured work lists live outside the rolling work FIFO, and the FIFO
+    steps persisted in device memory keep eager and replayed launches in
+    lock-step."""
+    import torch
+
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(n * 7 + 1)
+        send = [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)]
+        recv = [torch.empty_like(x) for x in send]
+        s = torch.cuda.Stream()
+        # warm-up outside capture (first launch loads the code object)
+        with C.group():
+            for r in range(n):
+                C.all_reduce(comms[r], send[r], recv[r], count, F16, 0, stream=s)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(2):  # two collectives in one graph
+                with C.group():
+                    for r in range(n):
+                        C.all_reduce(comms[r], send[r], recv[r], count, F16, 0, stream=s)
+        for it in range(3):
+            inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
+            for r in range(n):
+                send[r].copy_(torch.from_numpy(inputs[r]).cuda())
+            torch.cuda.synchronize()
+            if it == 1:  # an eager call between replays advances the same FIFOs
+                with C.group():
+                    for r in range(n):
+                        C.all_reduce(comms[r], send[r], recv[r], count, F16, 0, stream=s)
+                s.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            for c in comms:
+                c.sync()
+            exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0])
+            _check_all_equal([recv[r].cpu().numpy() for r in range(n)], exp, F16)
+    finally:
+        torch.cuda.synchronize()
+        vnode.destroy(comms)
