@@ -195,6 +195,29 @@ def _full_size_exact(torch, C, comm, rank, world, n, tdt, code, dev) -> bool:
     return ok
 
 
+def _graph_replay(torch, dist, comm, call_on, calls=10):
+    """Per-call time of `calls` AllReduces captured in one HIP graph (max over
+    ranks), after one untimed replay.  call_on(stream) issues one AllReduce."""
+    torch.cuda.synchronize()
+    gs = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=gs):
+        for _ in range(calls):
+            call_on(gs)
+    g.replay()
+    torch.cuda.synchronize()
+    comm.sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    comm.sync()
+    el = time.perf_counter() - t0
+    dist.barrier()
+    del g
+    return max_over_ranks(dist, el) / calls
+
+
 def _extra_fp16_1gib(torch, dist, C, comm, rank, world, dev, warmup=3, K=10):
     """BASELINE configs[3] on the communicator just measured: fp16 AllReduce
     of a 1 GiB bucket per rank, exact-sum validated at full size, algbw."""
@@ -334,6 +357,10 @@ def run(args):
         fallback = [m for m in _default_modes(C) if ("uncached" in m[0]) == bool(cached)]
         comm, mode = _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, full=(n, tdt, code),
                                           modes=fallback)
+    graph = None
+    if not getattr(args, "no_extra", False):
+        graph = _graph_replay(torch, dist, comm,
+                              lambda st: C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, st))
     del x, y
     extra = None
     if not getattr(args, "no_extra", False) and (dt_name, args.size_mib) == ("float32", 128):
@@ -391,6 +418,11 @@ def run(args):
         }
         if extra is not None:
             out["config"]["configs3_fp16_1GiB"] = extra
+        if graph is not None:
+            out["config"]["graph_replay"] = {
+                "ms_per_step": round(graph * 1e3, 4), "algbw_GBps": round(nbytes / graph / 1e9, 3),
+                "note": "the same AllReduce captured 10x in one HIP graph and replayed (no host path per call); "
+                        "value above is the eager path"}
         if not getattr(args, "no_cpu_baseline", False):
             out["cpu_ring_baseline"] = cpu_ring_baseline(C, world)
     comm.destroy()

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bridge", type=int, default=0, help="CommConfig.bridge_streams (0 = library default)")
     ap.add_argument("--profile", action="store_true", help="per-slice wait/stream timing (MCCS_RING_PROFILE)")
+    ap.add_argument("--graph", action="store_true", help="also time the same calls captured in one HIP graph")
     args = ap.parse_args()
     if args.profile:
         os.environ["MCCS_RING_PROFILE"] = "1"
@@ -58,9 +59,29 @@ def main():
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / args.iters
                 prof = C.ring_profile(0, reset=True) if args.profile else None
+                graph_ms = None
+                if args.graph:  # the same iters calls as one graph replay (no host path per call)
+                    st = torch.cuda.Stream()
+                    g = torch.cuda.CUDAGraph()
+                    torch.cuda.synchronize()
+                    with torch.cuda.graph(g, stream=st):
+                        for _ in range(args.iters):
+                            with C.group():
+                                for r in range(n):
+                                    C.all_reduce(comms[r], xs[r], ys[r], cnt, C.AllReduceDataType.Float32, stream=st)
+                    g.replay()
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    g.replay()
+                    torch.cuda.synchronize()
+                    graph_ms = (time.perf_counter() - t0) / args.iters * 1e3
+                    del g
                 print(json.dumps({"n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels,
                                   "block": comms[0].block_threads, "bridge": args.bridge, "MiB": mib, "ms": round(dt * 1e3, 3),
-                                  "algbw_GBps": round((mib << 20) / dt / 1e9, 2), "slice_profile": prof}), flush=True)
+                                  "algbw_GBps": round((mib << 20) / dt / 1e9, 2), "slice_profile": prof,
+                                  "graph_ms": round(graph_ms, 4) if graph_ms else None,
+                                  "graph_algbw_GBps": round((mib << 20) / graph_ms / 1e6, 2) if graph_ms else None}),
+                      flush=True)
                 del xs, ys
             torch.cuda.synchronize()
             for c in comms:
