@@ -242,6 +242,30 @@ def _extra_fp16_1gib(torch, dist, C, comm, rank, world, dev, warmup=3, K=10):
             "validated_exact_sum_full_size": ok}
 
 
+def _extra_allgather(torch, dist, C, comm, rank, world, dev, mib=16, warmup=3, K=10):
+    """The other reachable collective (all_gather.h): AllGather of `mib` MiB
+    per rank on the same communicator; every gathered segment checked byte
+    for byte.  algbw = gathered bytes / t (nccl-tests convention)."""
+    nb = mib << 20
+    i = torch.arange(nb, device=dev, dtype=torch.int32)
+    x = ((i * 31 + rank * 101) % 251).to(torch.uint8)
+    y = torch.empty(world * nb, dtype=torch.uint8, device=dev)
+
+    def step():
+        C.all_gather(comm, x, y, nb)
+
+    el = max_over_ranks(dist, _time_steps(torch, dist, comm, step, warmup, K))
+    ok = all(bool(torch.equal(y[r * nb:(r + 1) * nb], ((i * 31 + r * 101) % 251).to(torch.uint8)))
+             for r in range(world))
+    ok = agree(dist, ok)
+    per = el / K
+    algbw = world * nb / per / 1e9
+    del x, y, i
+    torch.cuda.empty_cache()
+    return {"ms_per_step": round(per * 1e3, 4), "algbw_GBps": round(algbw, 3),
+            "busbw_GBps": round(algbw * (world - 1) / world, 3), "steps": K, "validated_bytes": ok}
+
+
 def _out_links(rings, rank):
     """Distinct xGMI links this rank sends on (one per distinct ring successor)."""
     nxt = set()
@@ -362,9 +386,10 @@ def run(args):
         graph = _graph_replay(torch, dist, comm,
                               lambda st: C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, st))
     del x, y
-    extra = None
+    extra = gather = None
     if not getattr(args, "no_extra", False) and (dt_name, args.size_mib) == ("float32", 128):
         extra = _extra_fp16_1gib(torch, dist, C, comm, rank, world, dev)
+        gather = _extra_allgather(torch, dist, C, comm, rank, world, dev)
     algbw = nbytes / per_step / 1e9
     busbw = algbw * 2 * (world - 1) / world
     link_bytes = 2 * (world - 1) / world * nbytes
@@ -418,6 +443,8 @@ def run(args):
         }
         if extra is not None:
             out["config"]["configs3_fp16_1GiB"] = extra
+        if gather is not None:
+            out["config"]["allgather_16MiB_per_rank"] = gather
         if graph is not None:
             out["config"]["graph_replay"] = {
                 "ms_per_step": round(graph * 1e3, 4), "algbw_GBps": round(nbytes / graph / 1e9, 3),
