@@ -390,6 +390,13 @@ def run(args):
     if not getattr(args, "no_extra", False) and (dt_name, args.size_mib) == ("float32", 128):
         extra = _extra_fp16_1gib(torch, dist, C, comm, rank, world, dev)
         gather = _extra_allgather(torch, dist, C, comm, rank, world, dev)
+    setup2 = None
+    if (not getattr(args, "no_extra", False) and world % 2 == 0
+            and world >= int(os.environ.get("MCCS_BENCH_SETUP2_MIN_WORLD", "8"))):
+        # BASELINE configs[4] on a full node: the two jobs on disjoint halves
+        _, jobs2, _ = _setup2_measure(torch, dist, C, rank, world, device, dev, False, 3, 10)
+        setup2 = {"workload": "2 concurrent allreduce jobs, setup-2 shapes (BASELINE configs[4]), disjoint halves",
+                  "jobs": jobs2, "steps": 10}
     algbw = nbytes / per_step / 1e9
     busbw = algbw * 2 * (world - 1) / world
     link_bytes = 2 * (world - 1) / world * nbytes
@@ -445,6 +452,8 @@ def run(args):
             out["config"]["configs3_fp16_1GiB"] = extra
         if gather is not None:
             out["config"]["allgather_16MiB_per_rank"] = gather
+        if setup2 is not None:
+            out["config"]["configs4_two_jobs"] = setup2
         if graph is not None:
             out["config"]["graph_replay"] = {
                 "ms_per_step": round(graph * 1e3, 4), "algbw_GBps": round(nbytes / graph / 1e9, 3),
@@ -470,11 +479,9 @@ def setup2_jobs(world: int, interleaved: bool) -> list[list[int]]:
     return [list(range(0, world // 2)), list(range(world // 2, world))]
 
 
-def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False):
-    """BASELINE configs[4]: two concurrent AllReduce jobs on the node, shapes
-    from workloads/setup-2_{vgg,gpt_1}.toml.  Each job times its own K calls;
-    both run at the same time (traffic_gen/src/main.rs:167-228 reports each
-    job's per-iteration time the same way)."""
+def _setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup, steps):
+    """Both setup-2 jobs at once (one communicator per job on its half of the
+    node); returns (members, per-job dicts, fifo mode) on every rank."""
     members = setup2_jobs(world, interleaved)
     groups = [dist.new_group(m) for m in members]
     job = 0 if rank in members[0] else 1
@@ -494,22 +501,34 @@ def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False
         C.all_reduce(comm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum)
 
     dist.barrier()  # both jobs start together
-    el = _time_steps(torch, dist, comm, step, args.warmup, args.steps, grp)
+    el = _time_steps(torch, dist, comm, step, warmup, steps, grp)
     t = torch.tensor([el], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
     per_job = torch.zeros(2, dtype=torch.float64)
-    per_job[job] = t[0] / args.steps
+    per_job[job] = t[0] / steps
     dist.all_reduce(per_job, op=dist.ReduceOp.MAX)
     comm.destroy()
+    del x, y
+    torch.cuda.empty_cache()
     dist.barrier()
-    dist.destroy_process_group()
-    if rank != 0:
-        return None
     jobs = []
     for j, (nm, cnt) in enumerate(SETUP2_JOBS):
         ps = float(per_job[j])
         jobs.append({"job": nm, "ranks": half, "bytes": cnt * 2, "ms_per_call": round(ps * 1e3, 4),
                      "algbw_GBps": round(cnt * 2 / ps / 1e9, 3)})
+    return members, jobs, mode
+
+
+def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False):
+    """BASELINE configs[4]: two concurrent AllReduce jobs on the node, shapes
+    from workloads/setup-2_{vgg,gpt_1}.toml.  Each job times its own K calls;
+    both run at the same time (traffic_gen/src/main.rs:167-228 reports each
+    job's per-iteration time the same way)."""
+    members, jobs, mode = _setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, args.warmup,
+                                          args.steps)
+    dist.destroy_process_group()
+    if rank != 0:
+        return None
     return {
         "metric": "device-resident reduce GB/s; ring-allreduce algbw GB/s at 1/2/4/8 MI355X",
         "submetric": "concurrent_jobs_algbw_GBps",
