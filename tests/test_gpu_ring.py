@@ -340,8 +340,8 @@ def test_ring_profile_counters(monkeypatch):
         C.init_all([0])[0].destroy()  # disarm
 
 
-@pytest.mark.parametrize("n,count", [(2, 1 << 20), (4, 300007)])
-def test_allreduce_captured_in_hip_graph(orc, n, count):
+@pytest.mark.parametrize("n,count,bridge", [(2, 1 << 20, None), (4, 300007, None), (2, 77777, 1)])
+def test_allreduce_captured_in_hip_graph(orc, n, count, bridge):
     """AllReduces captured into a HIP graph (torch.cuda.graph) replay with the
     inputs of each replay, interleaved with eager calls on the same comms:
     captured work lists live outside the rolling work FIFO, and the FIFO
@@ -349,7 +349,9 @@ def test_allreduce_captured_in_hip_graph(orc, n, count):
     lock-step."""
     import torch
 
-    comms = C.init_all([0] * n)
+    # bridge=1: launches go to the comm's own stream, joined to the capturing
+    # stream by events (libmccs two-stream bridge)
+    comms = C.init_all([0] * n, C.CommConfig(bridge_streams=bridge))
     try:
         rng = np.random.default_rng(n * 7 + 1)
         send = [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)]
