@@ -387,3 +387,48 @@ def test_allreduce_captured_in_hip_graph(orc, n, count, bridge):
     finally:
         torch.cuda.synchronize()
         vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("code,off", [(F16, 2), (F32, 4), (F32, 12), (BF16, 6)])
+def test_allreduce_misaligned_buffers(orc, code, off):
+    """User buffers that are not 16-byte aligned take the typed element path
+    of the reduce-copy (common_kernel.h:485-550 ReduceCopyMulti) in every
+    primitive; results stay bit-identical to the oracle."""
+    import torch
+
+    n, count = 3, 100003
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(off * 10 + code)
+        inputs = [vnode.gen(code, count, rng) for _ in range(n)]
+        nbytes = inputs[0].nbytes
+        sbuf = [torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        rbuf = [torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        for r in range(n):
+            sbuf[r][off:off + nbytes].copy_(torch.from_numpy(inputs[r].view(np.uint8).copy()).cuda())
+        with C.group():
+            for r in range(n):
+                C.all_reduce(comms[r], sbuf[r].data_ptr() + off, rbuf[r].data_ptr() + off, count, code, 0)
+        for c in comms:
+            c.sync()
+        outs = [rbuf[r][off:off + nbytes].cpu().numpy().view(inputs[0].dtype) for r in range(n)]
+        exp = vnode.expected_allreduce(orc, inputs, code, 0, comms[0])
+        _check_all_equal(outs, exp, code)
+    finally:
+        vnode.destroy(comms)
+
+
+def test_allreduce_zero_count_is_noop():
+    import torch
+
+    comms = C.init_all([0, 0])
+    try:
+        x = torch.ones(4, device="cuda")
+        with C.group():
+            for c in comms:
+                C.all_reduce(c, x, x, 0, F32, 0)
+        for c in comms:
+            c.sync()
+        assert torch.equal(x, torch.ones(4, device="cuda"))
+    finally:
+        vnode.destroy(comms)
