@@ -99,8 +99,8 @@ typedef struct mccsComm *mccsComm_t;
 typedef struct {
   int channel_count;    /* rings; 0 = auto: 2 x edge-disjoint Hamiltonian cycles of the node */
   int buffer_size;      /* FIFO bytes per connection (buffer_sizes[0]); 0 = 4 MiB */
-  int lanes;            /* workgroups per channel; 0 = auto (~48 per rank, fitted to residency) */
-  int block_threads;    /* threads per workgroup (64..1024); 0 = 512 */
+  int lanes;            /* workgroups per channel; 0 = auto (64 / channels, <= 16, fitted to residency) */
+  int block_threads;    /* threads per workgroup (64..576, multiple of 32); 0 = 512 */
   int locality;         /* MCCS_LOCALITY_*; default RECEIVER (remote writes; SENDER = reference shm layout) */
   int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED */
   int timeout_ms;       /* FIFO spin watchdog; 0 = 30000, < 0 = never */

@@ -96,6 +96,35 @@ def build_lib(verbose: bool = False, jobs: int | None = None) -> str:
     return LIB
 
 
+CAPI_SRC = os.path.join(ROOT, "tests", "capi", "capi_allreduce.c")
+CAPI_BIN = os.path.join(ROOT, "tests", "capi", "capi_allreduce")
+
+
+def capi_cmd(src: str, out: str, syntax_only: bool = False) -> list[str]:
+    """gcc (C11) against include/mccs_hip.h: the C-ABI as a non-C++ binding sees it."""
+    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Werror", f"-I{INCLUDE}", "-I/opt/rocm/include",
+           "-D__HIP_PLATFORM_AMD__", src]
+    if syntax_only:
+        return cmd + ["-fsyntax-only"]
+    return cmd + [f"-L{PKG}", "-lmccs_hip", "-L/opt/rocm/lib", "-lamdhip64",
+                  "-Wl,-rpath,$ORIGIN/../../mccs_amd", "-Wl,-rpath,/opt/rocm/lib", "-o", out]
+
+
+def build_capi(verbose: bool = False) -> str:
+    """tests/capi/capi_allreduce: plain-C driver of the C-ABI (run on the GPU by tests/test_gpu_capi.py)."""
+    build_lib(verbose=verbose)
+    if os.path.exists(CAPI_BIN) and os.path.getmtime(CAPI_BIN) >= max(os.path.getmtime(CAPI_SRC),
+                                                                        os.path.getmtime(LIB)):
+        return CAPI_BIN
+    cmd = capi_cmd(CAPI_SRC, CAPI_BIN)
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"C-ABI driver build failed:\n{r.stdout}\n{r.stderr}")
+    return CAPI_BIN
+
+
 def build_oracle(verbose: bool = False) -> None:
     """Builds oracle/libmccs_oracle.so (+ oracle/_ref when the reference tree exists)."""
     cmd = ["make", "-s", "-C", os.path.join(ROOT, "oracle")]
@@ -109,6 +138,7 @@ def build_oracle(verbose: bool = False) -> None:
 def main() -> None:
     verbose = "-v" in sys.argv
     print(build_lib(verbose=verbose))
+    build_capi(verbose=verbose)
     build_oracle(verbose=verbose)
 
 
