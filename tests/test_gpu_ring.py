@@ -432,3 +432,36 @@ def test_allreduce_zero_count_is_noop():
         assert torch.equal(x, torch.ones(4, device="cuda"))
     finally:
         vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("depth", [8, 16])
+def test_work_fifo_wraps_and_flow_controls(orc, depth):
+    """A tiny work FIFO (plan.rs:380-541: rolling work_queue indices, restart
+    at slot 0 on wrap, wait_work_queue on workFifoDone acks) over many calls:
+    every call's work list wraps the ring several times and the host must
+    wait for the kernel's acks before reusing slots."""
+    import torch
+
+    n = 2
+    comms = C.init_all([0] * n, C.CommConfig(work_fifo_depth=depth))
+    try:
+        rng = np.random.default_rng(depth)
+        counts = [1 << 16, 333, (1 << 18) + 7, 5]
+        outs_dev, exps = [], []
+        for it in range(40):  # ~40 calls x 2 channels >> depth: many wraps, issued back to back
+            count = counts[it % len(counts)]
+            inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
+            send = [vnode.to_dev(x) for x in inputs]
+            recv = [vnode.to_dev(np.zeros_like(x)) for x in inputs]
+            with C.group():
+                for r in range(n):
+                    C.all_reduce(comms[r], send[r], recv[r], count, F32, 0)
+            outs_dev.append((send, recv))
+            exps.append(vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
+        for c in comms:
+            c.sync()
+        torch.cuda.synchronize()
+        for (send, recv), exp in zip(outs_dev, exps):
+            _check_all_equal([vnode.from_dev(recv[r], F32) for r in range(n)], exp, F32)
+    finally:
+        vnode.destroy(comms)
