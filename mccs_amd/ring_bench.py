@@ -327,7 +327,11 @@ def run(args):
     torch.cuda.set_device(device)
     dev = torch.device("cuda", device)
     if not dist.is_initialized():
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import datetime
+
+        # a rank that dies mid-collective should end the job in minutes, not
+        # gloo's default 30
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
     if getattr(args, "jobs", None) in ("setup2", "setup2-interleaved"):
         return run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=args.jobs.endswith("interleaved"))
     exchange = _exchange_factory(dist, world)
