@@ -163,6 +163,10 @@ CONFIGS = [
     dict(channel_count=2, rings="default", block_threads=544, lanes=1),  # reference profile
     dict(channel_count=5),
     dict(bridge_streams=1),
+    # comm_patterns_override with rings that do not start at rank 0 and are
+    # not rotations of each other (ring.index relative to rank 0, userRanks)
+    dict(channel_count=2, rings=[[3, 0, 6, 1, 7, 2, 5, 4], [4, 5, 2, 7, 1, 6, 0, 3]]),
+    dict(channel_count=3, rings=[[5, 2, 0, 7, 4, 1, 6, 3]] * 3, lanes=2),
 ]
 
 
