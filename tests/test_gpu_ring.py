@@ -222,6 +222,30 @@ def test_allgather(orc, n, nbytes):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("cfg", [dict(channel_count=2, rings=[[3, 0, 6, 1, 7, 2, 5, 4], [4, 5, 2, 7, 1, 6, 0, 3]]),
+                                 dict(locality=C.LOCALITY_SENDER, lanes=3), dict(lanes=1, block_threads=544)])
+def test_allgather_configs(orc, cfg):
+    """AllGather (all_gather.h:7-79) under ring overrides (userRanks decide
+    every destination offset), sender-side FIFOs and the reference block."""
+    n, nbytes = 8, (3 << 20) + 11
+    comms = C.init_all([0] * n, C.CommConfig(**cfg))
+    try:
+        rng = np.random.default_rng(nbytes + len(str(cfg)))
+        inputs = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(n)]
+        send = [vnode.to_dev(x) for x in inputs]
+        recv = [vnode.to_dev(np.zeros(n * nbytes, np.uint8)) for _ in range(n)]
+        with C.group():
+            for r in range(n):
+                C.all_gather(comms[r], send[r], recv[r], nbytes)
+        for c in comms:
+            c.sync()
+        exp = orc.ring_allgather(inputs)
+        for r in range(n):
+            assert np.array_equal(recv[r].cpu().numpy(), exp), r
+    finally:
+        vnode.destroy(comms)
+
+
 def test_fused_launch_beyond_residency_fails_loudly():
     """Explicit lanes whose fused vnode launch cannot be co-resident would
     deadlock (every block spins on a peer's flag): refused, not hung."""
