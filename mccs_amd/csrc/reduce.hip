@@ -158,29 +158,24 @@ __device__ __forceinline__ void wait_younger(int nd, int ns) {
 
 // One lane's 16 bytes of a wave-wide LDS-DMA: LDS dst = M0 + lane*16.
 // NT: non-temporal (streaming) policy on the DMA read.
-template <bool NT>
+template <int POL>
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_wave_base) {
   uint32_t keep;
-  if constexpr (NT)
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off nt\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_wave_base)
-        : "memory");
-  else
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_wave_base)
-        : "memory");
+#define MCCS_GLDS(MODS)                                                   \
+  asm volatile(                                                           \
+      "s_mov_b32 %0, m0\n\t"                                              \
+      "s_mov_b32 m0, %2\n\t"                                              \
+      "s_nop 0\n\t"                                                       \
+      "global_load_lds_dwordx4 %1, off " MODS "\n\t"                      \
+      "s_mov_b32 m0, %0"                                                  \
+      : "=&s"(keep)                                                       \
+      : "v"(gsrc), "s"(lds_wave_base)                                     \
+      : "memory")
+  if constexpr (POL == kNonTemporal) MCCS_GLDS("nt");
+  else if constexpr (POL == kNtWriteThrough) MCCS_GLDS("sc1 nt");
+  else if constexpr (POL == kSystemNt) MCCS_GLDS("sc0 sc1 nt");
+  else MCCS_GLDS("");
+#undef MCCS_GLDS
 }
 
 template <int DT, int OP, int U, int S, int W, int LDP, int STP>
@@ -208,8 +203,8 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
     for (int u = 0; u < U; ++u) {
       int64_t p = tile * wtile + u * 64 + lane;
       p = p < npack ? p : npack - 1;  // clamp: partial last tile re-reads a valid pack
-      glds16<LDP == kNonTemporal>(s0 + p, base + u * 1024);
-      glds16<LDP == kNonTemporal>(s1 + p, base + (U + u) * 1024);
+      glds16<LDP>(s0 + p, base + u * 1024);
+      glds16<LDP>(s1 + p, base + (U + u) * 1024);
     }
   };
 
@@ -339,7 +334,7 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
   const size_t lds = (size_t)W * S * 2 * U * 1024;
   // pol: 0 plain DMA + plain stores, 1 nt DMA + nt stores, 2 plain DMA + nt
   // stores; nt DMA with write-through stores (tuning grid only): 3 nt+sc1,
-  // 4 sc1, 5 sc0+sc1+nt
+  // 4 sc1, 5 sc0+sc1+nt; sc1 stores with 6 "sc1 nt" / 7 "sc0 sc1 nt" DMA reads
   auto kn = reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNonTemporal>;
   auto kp = reduce_lds_kernel<DT, OP, U, S, W, kPlain, kPlain>;
   auto ks = reduce_lds_kernel<DT, OP, U, S, W, kPlain, kNonTemporal>;
@@ -352,10 +347,12 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
   }
   if constexpr (tuned_grid<DT, OP>() && U == 4 && S == 3 && W == 4) {
     if (pol >= 3) {
-      auto kw = pol == 3 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNtWriteThrough>
+      auto kw = pol == 3   ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNtWriteThrough>
                 : pol == 4 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kWriteThrough>
-                           : reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kSystemNt>;
-      static std::atomic<unsigned> wt_attr_set{0};  // bit per policy 3..5
+                : pol == 5 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kSystemNt>
+                : pol == 6 ? reduce_lds_kernel<DT, OP, U, S, W, kNtWriteThrough, kWriteThrough>
+                           : reduce_lds_kernel<DT, OP, U, S, W, kSystemNt, kWriteThrough>;
+      static std::atomic<unsigned> wt_attr_set{0};  // bit per policy 3..7
       const unsigned bit = 1u << (pol - 3);
       if (!(wt_attr_set.load(std::memory_order_relaxed) & bit)) {
         (void)hipFuncSetAttribute((const void*)kw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -496,7 +493,7 @@ extern "C" mccsResult_t mccs_hip_reduce(void* dst, const void* const* srcs, int 
 extern "C" mccsResult_t mccs_hip_reduce_tune(int variant, int unroll, int policy, int blocks_per_cu,
                                              int stages, int waves) {
   if (variant < 0 || variant > MCCS_REDUCE_VARIANT_REG_ROWS) return mccsInvalidArgument;
-  if (policy > 5) return mccsInvalidArgument;
+  if (policy > 7) return mccsInvalidArgument;
   if (unroll < 0 || unroll > 8 || (unroll & (unroll - 1))) return mccsInvalidArgument;
   if (stages < 0 || stages == 1 || stages > 4 || waves < 0 || (waves != 0 && (waves < 4 || waves > 8 || waves == 7)))
     return mccsInvalidArgument;
