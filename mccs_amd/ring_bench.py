@@ -266,6 +266,34 @@ def _extra_allgather(torch, dist, C, comm, rank, world, dev, mib=16, warmup=3, K
             "busbw_GBps": round(algbw * (world - 1) / world, 3), "steps": K, "validated_bytes": ok}
 
 
+# the reference's evaluation sweep (eval/plot/single_app/allreduce_{4,8}gpu.csv:
+# fp16 "half", 32 KiB ... 512 MiB)
+SWEEP_BYTES = (32768, 131072, 524288, 2097152, 8388608, 33554432, 134217728, 536870912)
+
+
+def _size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20):
+    """fp16 AllReduce latency / algbw / busbw over the reference's eval sizes
+    (allreduce_bench semantics: algbw = bytes / t, busbw = algbw * 2(n-1)/n),
+    each size exact-sum validated."""
+    rows = []
+    for nb in SWEEP_BYTES:
+        n = nb // 2
+        x = torch.empty(n, dtype=torch.float16, device=dev).uniform_(-1, 1)
+        y = torch.empty_like(x)
+
+        def step():
+            C.all_reduce(comm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum)
+
+        el = max_over_ranks(dist, _time_steps(torch, dist, comm, step, warmup, K)) / K
+        del x, y
+        ok = agree(dist, _full_size_exact(torch, C, comm, rank, world, n, torch.float16,
+                                          C.AllReduceDataType.Float16, dev))
+        algbw = nb / el / 1e9
+        rows.append({"bytes": nb, "latency_us": round(el * 1e6, 2), "algbw_GBps": round(algbw, 3),
+                     "busbw_GBps": round(algbw * 2 * (world - 1) / world, 3), "exact": ok})
+    return rows
+
+
 def _out_links(rings, rank):
     """Distinct xGMI links this rank sends on (one per distinct ring successor)."""
     nxt = set()
@@ -390,10 +418,11 @@ def run(args):
         graph = _graph_replay(torch, dist, comm,
                               lambda st: C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, st))
     del x, y
-    extra = gather = None
+    extra = gather = sweep = None
     if not getattr(args, "no_extra", False) and (dt_name, args.size_mib) == ("float32", 128):
         extra = _extra_fp16_1gib(torch, dist, C, comm, rank, world, dev)
         gather = _extra_allgather(torch, dist, C, comm, rank, world, dev)
+        sweep = _size_sweep(torch, dist, C, comm, rank, world, dev)
     setup2 = None
     if (not getattr(args, "no_extra", False) and world % 2 == 0
             and world >= int(os.environ.get("MCCS_BENCH_SETUP2_MIN_WORLD", "8"))):
@@ -456,6 +485,8 @@ def run(args):
             out["config"]["configs3_fp16_1GiB"] = extra
         if gather is not None:
             out["config"]["allgather_16MiB_per_rank"] = gather
+        if sweep is not None:
+            out["config"]["size_sweep_fp16"] = sweep
         if setup2 is not None:
             out["config"]["configs4_two_jobs"] = setup2
         if graph is not None:
