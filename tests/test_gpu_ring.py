@@ -82,6 +82,25 @@ def test_allreduce_ops(orc, op, code):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("code", list(range(10)))
+@pytest.mark.parametrize("op", [0, 2])
+def test_allreduce_every_dtype(orc, code, op):
+    """All ten mccsDevDataType_t kernels (collectives.h:177-192; the reference
+    compiled them, libmccs reached two) through the ring, Sum and Max, n = 3
+    (non-commutative fp order), ragged count: bit-exact vs the oracle.  Byte
+    types run the 4-pack reduce-copy, 64-bit types two elements per pack."""
+    n, count = 3, 250007
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(code * 10 + op)
+        inputs = [vnode.gen(code, count, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, code, op)
+        exp = vnode.expected_allreduce(orc, inputs, code, op, comms[0])
+        _check_all_equal(outs, exp, code)
+    finally:
+        vnode.destroy(comms)
+
+
 @pytest.mark.parametrize("count", [1, 7, 255, 256, 4097, 1 << 20, 5 * (1 << 19) // 2 + 77, (3 << 20) + 5])
 def test_allreduce_sizes(orc, count):
     n = 4
