@@ -217,3 +217,20 @@ def test_reduce_captured_in_hip_graph(orc):
     for k in range(3):
         (ref,) = orc.reduce_copy(7, 0, [srcs[k][0].cpu().numpy(), hs[k][1]])
         assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), ref.view(np.uint32)), k
+
+
+def test_reduce_beyond_2pow31_elements():
+    """Maximum-size edge for the standalone chunk reduce: uint8 2^31 + 17
+    elements (64-bit pack and tile indices, partial last tile, byte tail)."""
+    import mccs_amd
+    import torch
+
+    n = (1 << 31) + 17
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    a = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    b = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    c = torch.empty_like(a)
+    mccs_amd.reduce(c, [a, b])
+    torch.cuda.synchronize()
+    assert torch.equal(c, a + b)

@@ -512,3 +512,31 @@ def test_work_fifo_wraps_and_flow_controls(orc, depth):
             _check_all_equal([vnode.from_dev(recv[r], F32) for r in range(n)], exp, F32)
     finally:
         vnode.destroy(comms)
+
+
+def test_allreduce_beyond_2pow31_elements():
+    """Maximum-size edge: an int8 AllReduce of 2^31 + 5 elements per rank
+    (64-bit offsets through the chunk schedule, the work element's count and
+    the lane split), checked against a wrapping int8 sum on the device."""
+    import torch
+
+    n, count = 2, (1 << 31) + 5
+    comms = C.init_all([0] * n)
+    try:
+        g = torch.Generator(device="cuda")
+        xs = []
+        for r in range(n):
+            g.manual_seed(100 + r)
+            xs.append(torch.randint(-8, 8, (count,), dtype=torch.int8, device="cuda", generator=g))
+        ys = [torch.empty_like(x) for x in xs]
+        with C.group():
+            for r in range(n):
+                C.all_reduce(comms[r], xs[r], ys[r], count, I8, 0)
+        for c in comms:
+            c.sync()
+        exp = xs[0] + xs[1]
+        for r in range(n):
+            assert torch.equal(ys[r], exp), r
+            assert ys[r][-5:].tolist() == exp[-5:].tolist()
+    finally:
+        vnode.destroy(comms)
