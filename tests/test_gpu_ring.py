@@ -540,3 +540,29 @@ def test_allreduce_beyond_2pow31_elements():
             assert ys[r][-5:].tolist() == exp[-5:].tolist()
     finally:
         vnode.destroy(comms)
+
+
+def test_allgather_output_beyond_2pow31_bytes():
+    """AllGather whose gathered output passes 2^31 bytes (destination offsets
+    rank * sendbytes in 64 bits, all_gather.h:29-79)."""
+    import torch
+
+    n, nb = 2, (3 << 29) + 3
+    comms = C.init_all([0] * n)
+    try:
+        g = torch.Generator(device="cuda")
+        xs = []
+        for r in range(n):
+            g.manual_seed(200 + r)
+            xs.append(torch.randint(0, 256, (nb,), dtype=torch.uint8, device="cuda", generator=g))
+        ys = [torch.empty(n * nb, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        with C.group():
+            for r in range(n):
+                C.all_gather(comms[r], xs[r], ys[r], nb)
+        for c in comms:
+            c.sync()
+        for r in range(n):
+            for s in range(n):
+                assert torch.equal(ys[r][s * nb:(s + 1) * nb], xs[s]), (r, s)
+    finally:
+        vnode.destroy(comms)
