@@ -23,7 +23,7 @@ def _check_all_equal(outs, exp, code):
         assert np.array_equal(o.view(np.uint8), exp.view(np.uint8)), f"rank {r} differs from oracle"
 
 
-@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("code", [F32, F16, BF16])
 def test_allreduce_matches_oracle(orc, n, code):
     comms = C.init_all([0] * n)
