@@ -28,7 +28,7 @@ def mean_counter(path, kernel_sub):
 def main():
     rtag = sys.argv[1]
     ptag = sys.argv[2] if len(sys.argv) > 2 else "reduce"
-    btag = sys.argv[3] if len(sys.argv) > 3 else "reduce_float32_128MiB_reduce_reg_kernel"
+    btag = sys.argv[3] if len(sys.argv) > 3 else "reduce_float32_128MiB_reduce_lds_kernel"
     os.makedirs(PROF, exist_ok=True)
     stats = os.path.join(OUT, f"prof_{ptag}_trace", "trace_kernel_stats.csv")
     dst = os.path.join(PROF, f"{rtag}_{ptag}_kernel_stats.csv")
