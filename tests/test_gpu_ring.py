@@ -566,3 +566,38 @@ def test_allgather_output_beyond_2pow31_bytes():
                 assert torch.equal(ys[r][s * nb:(s + 1) * nb], xs[s]), (r, s)
     finally:
         vnode.destroy(comms)
+
+
+def test_allgather_captured_in_hip_graph(orc):
+    """AllGather recorded into a HIP graph, replayed with new inputs."""
+    import torch
+
+    n, nbytes = 4, (1 << 20) + 9
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(77)
+        send = [torch.zeros(nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        recv = [torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        s = torch.cuda.Stream()
+        with C.group():
+            for r in range(n):
+                C.all_gather(comms[r], send[r], recv[r], nbytes, stream=s)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            with C.group():
+                for r in range(n):
+                    C.all_gather(comms[r], send[r], recv[r], nbytes, stream=s)
+        for _ in range(2):
+            inputs = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(n)]
+            for r in range(n):
+                send[r].copy_(torch.from_numpy(inputs[r]).cuda())
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            exp = orc.ring_allgather(inputs)
+            for r in range(n):
+                assert np.array_equal(recv[r].cpu().numpy(), exp), r
+    finally:
+        torch.cuda.synchronize()
+        vnode.destroy(comms)
