@@ -135,7 +135,7 @@ def _make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, gro
     return None, None
 
 
-def _autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for, warmup=2, reps=3):
+def _autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for, warmup=2, reps=6):
     """Transport placement chosen on the node itself: FIFO data at the
     receiver (remote writes) or at the sender (remote reads, the reference's
     SHM layout), each at the auto lane count and at 16 lanes per channel.
