@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--sweep-cfgs", default=None,
                     help="interleaved A/B of explicit configs 'v,u,pol,bpc,s,w;...' (stderr)")
     ap.add_argument("--sweep-rounds", type=int, default=5)
+    ap.add_argument("--sweep-launches", type=int, default=12, help="timed back-to-back launches per sweep sample")
     ap.add_argument("--no-autotune", action="store_true",
                     help="N>1: skip the on-node choice of FIFO placement / lanes (library defaults + fallbacks)")
     ap.add_argument("--no-extra", action="store_true",
@@ -175,7 +176,8 @@ def bench_reduce(args) -> dict:
     if args.sweep or args.sweep_reg or args.sweep_cfgs:
         # 'v,u,pol,bpc,s,w[,grid]' (grid: LDS grid cap, 0 = default)
         cfgs = [tuple(int(x) for x in c.split(",")) for c in args.sweep_cfgs.split(";")] if args.sweep_cfgs else None
-        sweep_variants(sets, n, code, stream, reg_only=args.sweep_reg, cfgs=cfgs, rounds=args.sweep_rounds)
+        sweep_variants(sets, n, code, stream, reg_only=args.sweep_reg, cfgs=cfgs, rounds=args.sweep_rounds,
+                       launches=args.sweep_launches)
 
     for _ in range(args.warmup):
         step()
@@ -268,7 +270,7 @@ def hbm_calibration(sets, n, code, stream) -> dict:
     return {"copy_1to1_GBps": round(2 * nb / t_copy / 1e9, 1)}
 
 
-def sweep_variants(sets, n, code, stream, reg_only=False, cfgs=None, rounds=5):
+def sweep_variants(sets, n, code, stream, reg_only=False, cfgs=None, rounds=5, launches=12):
     """Interleaved rounds of reduce variants in one process, rotating buffer
     sets like the timed loop (stderr)."""
     import torch
@@ -311,13 +313,13 @@ def sweep_variants(sets, n, code, stream, reg_only=False, cfgs=None, rounds=5):
                 mccs_amd.reduce(c_, [a_, b_], count=n, dtype=code, stream=stream)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(stream)
-            for _ in range(12):
+            for _ in range(launches):
                 a_, b_, c_ = sets[k % len(sets)]
                 k += 1
                 mccs_amd.reduce(c_, [a_, b_], count=n, dtype=code, stream=stream)
             e.record(stream)
             torch.cuda.synchronize()
-            times[cfg].append(s.elapsed_time(e) / 12)
+            times[cfg].append(s.elapsed_time(e) / launches)
     rows = sorted(((sorted(v)[len(v) // 2], min(v), cfg) for cfg, v in times.items()))
     for med, mn, cfg in rows:
         print(f"[sweep] variant={cfg[0]} unroll={cfg[1]} policy={cfg[2]} bpc={cfg[3]} stages={cfg[4]} "

@@ -250,21 +250,20 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
 
 // ---------------------------------------------------------------------------
 // Run-time configuration (process-wide; set before launches).  Defaults are
-// the fastest measured on MI355X with inputs streamed from HBM (bench.py
-// --sweep with buffer rotation, profiles/r01_*): the LDS-DMA loop with
-// non-temporal DMA reads and stores, 4 KiB per source per wave tile, a
-// 3-stage ring (double buffering plus one tile of slack), 4 waves, one block
-// per CU: 6.52 TB/s against 6.43 for the best REG loop on the same box.
-// Without nt on the DMA reads the same loop streams 5.9 TB/s.  Stores are
-// write-through (sc1), so no dirty lines wait in the XCD L2s for the
-// end-of-kernel writeback: +0.4 % over nt stores in 30-round A/Bs; see
-// DESIGN.md.
+// the fastest measured on MI355X in the regime bench.py times (50+
+// back-to-back launches, inputs streamed from HBM; bench.py --sweep-cfgs
+// --sweep-launches 60 on three boxes): the LDS-DMA loop, strict double
+// buffering (2 stages), 4 KiB per source per wave tile, 4 waves, one block
+// per CU, non-temporal DMA reads, write-through (sc1) stores.  It ties the
+// 3-stage nt-store ring and beats the best REG loop by ~1.2 %; the 3-stage
+// ring with sc1 stores, best in 12-launch bursts, is 1.3 % slower sustained.
+// Without nt on the DMA reads the loop streams 5.9 TB/s.  See DESIGN.md §3.1.
 struct ReduceTune {
   int variant = MCCS_REDUCE_VARIANT_LDS;
   int unroll = 4;  // LDS: 4 KiB per source per wave tile
   int policy = 4;  // nt LDS-DMA reads + write-through (sc1) stores; 1 = nt stores
-  int blocks_per_cu = 1;  // LDS: one 4-wave block per CU (96 KiB of LDS ring)
-  int stages = 3;
+  int blocks_per_cu = 1;  // LDS: one 4-wave block per CU (64 KiB of LDS ring)
+  int stages = 2;  // double buffer: one tile landing while the other is consumed
   int waves = 4;
 };
 static ReduceTune g_tune;
@@ -345,7 +344,7 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
     (void)hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set.store(true, std::memory_order_relaxed);
   }
-  if constexpr (tuned_grid<DT, OP>() && U == 4 && S == 3 && W == 4) {
+  if constexpr (tuned_grid<DT, OP>() && U == 4 && (S == 2 || S == 3) && W == 4) {
     if (pol >= 3) {
       auto kw = pol == 3   ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kNtWriteThrough>
                 : pol == 4 ? reduce_lds_kernel<DT, OP, U, S, W, kNonTemporal, kWriteThrough>
@@ -390,9 +389,9 @@ static hipError_t launch_lds_cfg(const ReduceArgs& a, const ReduceTune& t, bool*
   *ok = true;
 #define MCCS_LDS(U, S, W) \
   if (t.unroll == U && t.stages == S && t.waves == W) return launch_lds<DT, OP, U, S, W>(a, t.policy, t.blocks_per_cu, st);
-  MCCS_LDS(4, 3, 4)
+  MCCS_LDS(4, 2, 4)
   if constexpr (OP == OpSum && (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16)) {
-    MCCS_LDS(1, 3, 4) MCCS_LDS(2, 2, 4) MCCS_LDS(2, 3, 4) MCCS_LDS(4, 2, 4) MCCS_LDS(4, 4, 4) MCCS_LDS(8, 2, 4)
+    MCCS_LDS(1, 3, 4) MCCS_LDS(2, 2, 4) MCCS_LDS(2, 3, 4) MCCS_LDS(4, 3, 4) MCCS_LDS(4, 4, 4) MCCS_LDS(8, 2, 4)
     MCCS_LDS(4, 3, 5) MCCS_LDS(2, 3, 6) MCCS_LDS(4, 2, 6) MCCS_LDS(4, 3, 6)
     MCCS_LDS(1, 2, 8) MCCS_LDS(2, 2, 8) MCCS_LDS(4, 2, 8)
   }

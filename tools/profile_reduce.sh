@@ -10,7 +10,9 @@ OUT=$R/gpurun_out
 TAG=${PROF_TAG:-reduce}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-hot "$@")  # --no-hot: no same-buffer / copy-calibration launches of the same kernel
+# the bench's own defaults (50 timed steps after 10 warm-up); --no-hot: no
+# same-buffer (cache-assisted) launches of the same kernel in the average
+BENCH=(python3 "$R/bench.py" --no-cpu-baseline --no-hot "$@")
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_${TAG}_trace" -o trace \
   -- "${BENCH[@]}" > "$OUT/prof_${TAG}_trace.log" 2>&1 || { echo "trace pass failed $?"; exit 3; }
 for C in FETCH_SIZE WRITE_SIZE; do

@@ -56,6 +56,18 @@ def main():
         src = os.path.join(OUT, f"prof_{ptag}_{c}", "pmc_counter_collection.csv")
         if os.path.exists(src):
             shutil.copy(src, os.path.join(PROF, f"{rtag}_{ptag}_pmc_{c}.csv"))
+    # the bench's timed region = the last `steps` launches of the kernel
+    steps = int(os.environ.get("PROF_STEPS", "50"))
+    trace = os.path.join(OUT, f"prof_{ptag}_trace", "trace_kernel_trace.csv")
+    if os.path.exists(trace):
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                for r in csv.DictReader(open(trace)) if kname in r["Kernel_Name"]]
+        timed = durs[-steps:]
+        if timed and btag in d:
+            d[btag]["timed_region_avg_us"] = round(sum(timed) / len(timed), 3)
+            d[btag]["timed_region_launches"] = len(timed)
+            d[btag]["all_launches_avg_us"] = round(sum(durs) / len(durs), 3)
+            json.dump(d, open(tj, "w"), indent=1, sort_keys=True)
     print(open(dst).read())
     print(json.dumps(d.get(btag), indent=1))
 
