@@ -52,7 +52,13 @@ def main():
         fifo, loc = all_modes[mode]
         comm = C.init_communicator_rank(rank, world, dev, exchange,
                                         C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000))
-        for code, count in ((2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)):
+        cases = [(2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)]
+        nfuzz = int(os.environ.get("IPC_FUZZ", "0"))
+        if nfuzz:  # seeded random dtypes / ragged counts, same on every rank
+            frng = np.random.default_rng(4242)
+            cases = [(int(frng.choice([0, 2, 4, 6, 7, 8, 9])), int(frng.choice([1, 5, 4099, int(frng.integers(1, 3 << 20))])))
+                     for _ in range(nfuzz)]
+        for code, count in cases:
             rng = np.random.default_rng(count * 31 + rank)
             x = vnode.gen(code, count, rng)
             if code == 2:
