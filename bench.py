@@ -69,7 +69,7 @@ def cpu_threads() -> int:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))  # the GPU box's CPU share is 16 per GPU
+    return max(1, n)  # every hardware thread this process may run on (the GPU box pins a 16-thread share)
 
 
 def cpu_baseline(dtype_code: int, nelem: int, budget_s: float) -> dict:
@@ -110,6 +110,33 @@ def cpu_baseline(dtype_code: int, nelem: int, budget_s: float) -> dict:
                   f"on {nthr} threads; 1-thread {res['st'][0]:.3f} GB/s ({res['st'][2]} passes)",
         "single_thread_value": round(res["st"][0], 3),
     }
+
+
+def host_loopback_latency(calls: int = 200) -> dict:
+    """BASELINE configs[0]: 2-rank loopback AllReduce of 1 KiB fp32 on host
+    threads (mccs_host_ring_allreduce: the ring protocol over host memory,
+    reference schema 1 channel x 96 threads).  Median wall time per call over
+    `calls` calls; the result is checked against a + b (n = 2: exact)."""
+    import numpy as np
+
+    from mccs_amd import comm as C
+
+    rng = np.random.default_rng(0x6D636373)
+    send = [(rng.random(256, dtype=np.float32) * 2 - 1) for _ in range(2)]
+    recv = [np.empty_like(x) for x in send]
+    ts = []
+    for i in range(calls + 10):
+        t0 = time.perf_counter()
+        C.host_ring_allreduce(send, recv, 256, C.AllReduceDataType.Float32, channels=1, nthreads=96)
+        if i >= 10:
+            ts.append(time.perf_counter() - t0)
+    exp = send[0] + send[1]
+    if not all(np.array_equal(r, exp) for r in recv):
+        raise SystemExit("configs[0] host loopback: result mismatch")
+    ts.sort()
+    return {"workload": "2-rank loopback allreduce, 1 KiB fp32, host-side sum (BASELINE configs[0])",
+            "median_us": round(ts[len(ts) // 2] * 1e6, 2), "p10_us": round(ts[len(ts) // 10] * 1e6, 2),
+            "p90_us": round(ts[9 * len(ts) // 10] * 1e6, 2), "calls": calls, "exact": True}
 
 
 def load_pmc_traffic(tag: str):
@@ -363,6 +390,7 @@ def main():
                     "bfloat16": DataType.Bfloat16}[args.dtype]
             esz = 2 if args.dtype != "float32" else 4
             out["cpu_baseline"] = cpu_baseline(int(code), (args.size_mib << 20) // esz, args.cpu_seconds)
+            out["config"]["configs0_host_loopback_1KiB"] = host_loopback_latency()
         else:
             out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)

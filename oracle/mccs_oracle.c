@@ -358,6 +358,20 @@ static void reduce_range(const struct mt_job *j) {
     for (size_t i = 0; i < n; ++i) c[i] = a[i] + b[i];
     return;
   }
+  if (j->dtype == T_F32 && j->op == OP_SUM && j->nsrcs > 2) {
+    /* n-source sum in L1-sized blocks: every source read once, dst written once */
+    float *c = (float *)dst;
+    for (size_t b = 0; b < n; b += 2048) {
+      const size_t m = n - b < 2048 ? n - b : 2048;
+      const float *a0 = (const float *)s0 + b;
+      for (size_t i = 0; i < m; ++i) c[b + i] = a0[i];
+      for (int k = 1; k < j->nsrcs; ++k) {
+        const float *ak = (const float *)j->srcs[k] + j->lo + b;
+        for (size_t i = 0; i < m; ++i) c[b + i] = ak[i] + c[b + i];
+      }
+    }
+    return;
+  }
   if (dst != s0) memcpy(dst, s0, n * es);
   for (int i = 1; i < j->nsrcs; ++i)
     oracle_apply(j->dtype, j->op, dst, dst, (const char *)j->srcs[i] + j->lo * es, n);

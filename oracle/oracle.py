@@ -47,6 +47,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_float_to_half.restype = ctypes.c_uint16
         L.oracle_float_to_bf16.argtypes = [ctypes.c_float]
         L.oracle_float_to_bf16.restype = ctypes.c_uint16
+        L.oracle_verifiable_float_sum.argtypes = [ci, ci, ci, ci, ctypes.c_uint64, ctypes.c_int64, sz, ci, vp]
+        L.oracle_sum_float_tolerance.argtypes = [ci, ci]
+        L.oracle_sum_float_tolerance.restype = ctypes.c_uint
         _lib = L
     return _lib
 
@@ -114,3 +117,27 @@ def ring_allgather(inputs: list[np.ndarray]) -> np.ndarray:
     outs = (ctypes.c_void_p * n)(*([out.ctypes.data] * n))
     assert lib().oracle_ring_allgather(n, _pa(inputs), outs, inputs[0].size) == 0
     return out
+
+
+def verifiable_sum(dtype: int, nranks: int, count: int, seed: int, index0: int = 0, same_sign: bool = False):
+    """nccl-tests verifiable float-sum vectors (verifiable.c restates
+    verifiable.cu:466-512, 664-676): returns (inputs per rank, expected sum);
+    the inputs sum exactly to the expected value in any order."""
+    npdt = NP_DTYPE[dtype]
+    ins = []
+    for r in range(nranks):
+        x = np.empty(count, dtype=npdt)
+        rc = lib().oracle_verifiable_float_sum(dtype, 1, nranks, r, seed, index0, count, int(same_sign),
+                                               x.ctypes.data)
+        assert rc == 0, rc
+        ins.append(x)
+    y = np.empty(count, dtype=npdt)
+    rc = lib().oracle_verifiable_float_sum(dtype, 0, nranks, 0, seed, index0, count, int(same_sign), y.ctypes.data)
+    assert rc == 0, rc
+    return ins, y
+
+
+def sum_float_tolerance(nranks: int, dtype: int) -> int:
+    """calcSumFloatTolerance (verifiable.cu:981-1004): max bit distance of an
+    inexact n-term float sum from the correctly rounded one."""
+    return int(lib().oracle_sum_float_tolerance(nranks, dtype))

@@ -9,6 +9,12 @@ ring_golden.npz  small ring-allreduce vectors: inputs and the expected output,
                  produced by the C oracle and accepted only if the independent
                  per-rank FIFO simulation (tests/ring_sim.py) agrees bit for
                  bit.  Regression vectors for the oracle and GPU parity tests.
+                 Exact-sum cases ("verifiable") take their inputs and
+                 expected sum from the nccl-tests verifiable generator the
+                 reference vendors (genInOutFloatSum, verifiable.cu:466-512,
+                 restated in oracle/verifiable.c): the inputs sum exactly in
+                 any order, so the ring result must equal the generator's
+                 own output bit for bit -- a reference-held expected value.
 kat.json         allreduce_proto known answers (main.rs:111).
 """
 import json
@@ -41,7 +47,10 @@ CASES = {
     # name: (n, dtype, count, nch, nthreads, op, distribution)
     "loopback_1KiB_f32": (2, 7, 256, 1, 96, 0, "uniform"),
     "n4_f16_ragged": (4, 6, 20011, 2, 544, 0, "uniform"),
-    "n8_f16_exact": (8, 6, 20000, 2, 544, 0, "exact64"),
+    "n8_f16_verifiable": (8, 6, 20000, 2, 544, 0, "verifiable"),
+    "n4_f32_verifiable": (4, 7, 30011, 2, 544, 0, "verifiable"),
+    "n8_bf16_verifiable": (8, 9, 12345, 2, 544, 0, "verifiable"),
+    "n5_f16_verifiable_same_sign": (5, 6, 9999, 1, 160, 0, "verifiable_same_sign"),
     "n8_f32_uniform": (8, 7, 30011, 2, 544, 0, "uniform"),
     "n3_i32_prod": (3, 2, 5000, 1, 160, 1, "int"),
     "n4_bf16_sum": (4, 9, 10007, 2, 544, 0, "uniform"),
@@ -55,8 +64,8 @@ def gen_inputs(n, dtype, count, dist, seed):
     for _ in range(n):
         if dist == "int":
             out.append(rng.integers(-7, 8, count).astype(npdt))
-        elif dist == "exact64":
-            out.append((rng.integers(-255, 256, count) / 64.0).astype(npdt))
+        elif dist.startswith("verifiable"):
+            return orc.verifiable_sum(dtype, n, count, seed, same_sign=dist.endswith("same_sign"))[0]
         else:
             f = rng.random(count, dtype=np.float32) * 2 - 1
             out.append((f.view(np.uint32) >> 16).astype(np.uint16) if dtype == 9 else f.astype(npdt))
@@ -68,6 +77,9 @@ def ring_golden():
     for i, (name, (n, dtype, count, nch, nthr, op, dist)) in enumerate(sorted(CASES.items())):
         inputs = gen_inputs(n, dtype, count, dist, 1000 + i)
         out = orc.ring_allreduce(dtype, op, inputs, nchannels=nch, nthreads=nthr)
+        if dist.startswith("verifiable"):  # the generator's own expected sum, exact in any order
+            _, want = orc.verifiable_sum(dtype, n, count, 1000 + i, same_sign=dist.endswith("same_sign"))
+            assert np.array_equal(out.view(np.uint8), want.view(np.uint8)), name
         if dtype != 9:  # numpy has no bfloat16; bf16 cross-checked vs torch in tests
             sims = ring_sim.simulate(inputs, ["sum", "prod", "max", "min"][op], nch, nthr)
             for r in range(n):

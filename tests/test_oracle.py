@@ -222,3 +222,39 @@ def test_golden_ring_fixtures(orc):
         inputs = [z[f"{name}__in{r}"] for r in range(n)]
         got = orc.ring_allreduce(dtype, op, inputs, nchannels=nch, nthreads=nthr)
         assert np.array_equal(got.view(np.uint8), z[name + "__out"].view(np.uint8)), name
+
+
+def _as_f64(a, code):
+    if code == 9:
+        return (a.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    return a.astype(np.float64)
+
+
+@pytest.mark.parametrize("code", [6, 7, 8, 9])
+@pytest.mark.parametrize("same_sign", [False, True])
+def test_verifiable_generator_sums_exactly(orc, code, same_sign):
+    """genInOutFloatSum restatement (verifiable.cu:466-512): for every rank
+    count the inputs sum exactly (fp64 holds every partial sum) to the
+    generator's own expected output, and the ring oracle reproduces it in
+    its summation order bit for bit."""
+    for n in range(1, 9):
+        ins, want = orc.verifiable_sum(code, n, 30011, seed=977 + n, same_sign=same_sign)
+        assert np.array_equal(sum(_as_f64(x, code) for x in ins), _as_f64(want, code)), n
+        if n >= 2 and code != 8:
+            got = orc.ring_allreduce(code, 0, ins, nchannels=2, nthreads=544)
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), n
+
+
+def test_verifiable_generator_is_index_addressed(orc):
+    """Values depend only on (seed, index): generating a sub-range equals the
+    same slice of a full generation (so GPU tests can generate in parallel)."""
+    ins, want = orc.verifiable_sum(7, 8, 5000, seed=3)
+    ins2, want2 = orc.verifiable_sum(7, 8, 1000, seed=3, index0=2500)
+    assert np.array_equal(want[2500:3500], want2)
+    assert all(np.array_equal(a[2500:3500], b) for a, b in zip(ins, ins2))
+
+
+def test_nccl_sum_tolerance_values(orc):
+    # calcSumFloatTolerance (verifiable.cu:981-1004) at n = 2 / 4 / 8
+    assert [orc.sum_float_tolerance(n, 7) for n in (2, 4, 8)] == [2, 3, 4]
+    assert [orc.sum_float_tolerance(n, 6) for n in (2, 4, 8)] == [2, 3, 5]

@@ -1,4 +1,6 @@
 """CPU: host-side helpers of the multi-GPU bench leg (mccs_amd/ring_bench.py)."""
+import json
+
 import pytest
 
 from mccs_amd import comm as C
@@ -30,3 +32,48 @@ def test_setup2_shapes_match_workload_files():
 def test_workload_labels():
     assert rb.WORKLOADS[("float32", 128)].endswith("configs[2]")
     assert rb.WORKLOADS[("float16", 1024)].endswith("configs[3]")
+
+
+def _line(share, cpu=True):
+    return rb.ring_line(world=8, steps=20, warmup=5, per_step_s=1.2e-3, nbytes=128 << 20, dt_name="float32",
+                        comm_info={"channels": 6, "lanes": 10, "block_threads": 512},
+                        rings=C.default_rings(8), mode="receiver-uncached-fifo", tune_table=[], prof={},
+                        ranks_share_gpu=share,
+                        cpu_baseline=rb.cpu_sum_baseline(2, 1 << 20, budget_s=0.2) if cpu else None)
+
+
+@pytest.mark.parametrize("share", [False, True])
+def test_ring_line_schema(share):
+    """The N > 1 line carries the contract keys, a roofline whose frac is
+    achieved/peak <= 1 (HBM-bound when the ranks share one GPU) and a
+    non-null host baseline with its core count and host record."""
+    d = _line(share)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 8 and d["dtype"] == "f32" and d["scaling"] == "weak"
+    assert abs(d["value"] - (128 << 20) / 1.2e-3 / 1e9) < 1e-3
+    assert d["config"]["workload"].endswith("(BASELINE configs[2])")
+    rf = d["roofline"]
+    assert rf["bound"] == ("hbm" if share else "xgmi")
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and 0 < rf["frac"] <= 1
+    if share:
+        assert rf["peak"] == 8000.0 and abs(rf["achieved"] - 44 * (128 << 20) / 1.2e-3 / 1e9) < 0.01
+    else:
+        assert rf["peak"] == 6 * rb.XGMI_LINK_GBPS_PER_DIR
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    assert cb["host"]["affinity_threads"] >= 1 and "nproc" in cb["host"]
+    json.dumps(d)
+
+
+def test_rehearsal_roofline_never_above_one():
+    # the round-1 rehearsal (n = 2 on one GPU, 128 MiB in 0.43 ms) priced
+    # against xGMI gave frac 4; against the shared HBM it is below 1
+    rf = rb.ring_roofline(2, 128 << 20, 0.43e-3, 1, True, "k")
+    assert rf["bound"] == "hbm" and rf["frac"] < 1
+
+
+def test_bench_failure_is_nonzero_exit():
+    e = rb.BenchFailure("x")
+    assert isinstance(e, SystemExit) and e.code == "x"  # a non-int code exits with status 1
