@@ -8,6 +8,16 @@
  * stores as KernelPlan.kernel_fn); arguments are (comm, channelMask, workHead)
  * exactly as plan.rs:641-646 passes them.  Not for inclusion in HIP device
  * code (ring.hip defines these as extern "C" __global__).
+ *
+ * Reference linkage.  The reference declares the kernels with C++ linkage
+ * (collectives.h:49 has no extern "C"; collectives-sys/build.rs runs bindgen
+ * with "-x c++", so Rust binds the Itanium-mangled names) and names the bf16
+ * kernels after CUDA's type (..._<Op>___nv_bfloat16, common.h:182-188).  The
+ * library therefore also exports, at the same addresses:
+ *   _Z<len><name>P11mccsDevCommmP11mccsDevWork   for every name below, and
+ *   mccsKernel_AllReduce_RING_SIMPLE_<Op>___nv_bfloat16 (+ its mangled form)
+ * (link-time aliases, mccs_amd/build.py reference_aliases), so the
+ * reference's wrapper.h / collectives.h link against libmccs_hip.so as is.
  */
 #ifndef MCCS_AMD_KERNELS_H_
 #define MCCS_AMD_KERNELS_H_
@@ -64,6 +74,11 @@ MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Min_half);
 MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Min_float);
 MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Min_double);
 MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Min_bfloat16);
+/* the reference's bf16 spelling (same handles as the ..._bfloat16 ones) */
+MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Sum___nv_bfloat16);
+MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Prod___nv_bfloat16);
+MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Max___nv_bfloat16);
+MCCS_KERNEL_SYMBOL(mccsKernel_AllReduce_RING_SIMPLE_Min___nv_bfloat16);
 
 #ifdef __cplusplus
 }

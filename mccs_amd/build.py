@@ -76,6 +76,42 @@ def _compile(src: str, hdr_mtime: float, verbose: bool) -> str:
     return obj
 
 
+# Reference kernel names (collectives.h:43-49 MCCS_KERN_NAME, common.h:182-188)
+REF_OPS = ("Sum", "Prod", "Max", "Min")
+REF_TYPES = ("int8_t", "uint8_t", "int32_t", "uint32_t", "int64_t", "uint64_t", "half", "float", "double",
+             "bfloat16")
+
+
+def kernel_names() -> list[str]:
+    """The extern "C" kernel handles ring.hip defines."""
+    out = ["mccsKernel_AllGather_RING_SIMPLE_Sum_int8_t"]
+    for op in REF_OPS:
+        out += [f"mccsKernel_AllReduce_RING_SIMPLE_{op}_{t}" for t in REF_TYPES]
+    return out
+
+
+def cxx_mangled(name: str) -> str:
+    """Itanium mangling of the reference declaration (collectives.h:49):
+    void name(struct mccsDevComm*, uint64_t, struct mccsDevWork*)."""
+    return f"_Z{len(name)}{name}P11mccsDevCommmP11mccsDevWork"
+
+
+def reference_aliases() -> list[tuple[str, str]]:
+    """(alias, target) symbol pairs the link adds so the reference's own
+    collectives.h binds unchanged: the reference declares the kernels with
+    C++ linkage (no extern "C"; collectives-sys/build.rs runs bindgen with
+    -x c++), and names bf16 after CUDA's type, ..._<Op>___nv_bfloat16."""
+    pairs = []
+    for k in kernel_names():
+        names = [k]
+        if k.endswith("_bfloat16"):
+            nv = k[: -len("bfloat16")] + "__nv_bfloat16"
+            pairs.append((nv, k))
+            names.append(nv)
+        pairs += [(cxx_mangled(n), k) for n in names]
+    return pairs
+
+
 def build_lib(verbose: bool = False, jobs: int | None = None) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = _sources()
@@ -86,7 +122,8 @@ def build_lib(verbose: bool = False, jobs: int | None = None) -> str:
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
         tmp = LIB + ".tmp"
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lpthread"]
+        aliases = [f"-Wl,--defsym={a}={t}" for a, t in reference_aliases()]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lpthread", *aliases]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
