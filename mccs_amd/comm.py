@@ -252,11 +252,13 @@ def host_ring_allreduce(sendbufs, recvbufs, count: int, data_type, op_type=AllRe
 def ring_profile(device: int = 0, reset: bool = True) -> dict:
     """Per-slice timing of the ring kernels on `device` (MCCS_RING_PROFILE=1
     set before communicator init): slices, mean µs waiting for peer flags,
-    mean µs streaming + draining."""
+    mean µs streaming + draining (work_us), of which drain_us is the tail
+    after thread 0's wave issued its last store (store drain + barrier)."""
     out = (ctypes.c_ulonglong * 4)()
     _lib.check(_sig().mccs_ring_profile(device, out, 1 if reset else 0), "mccs_ring_profile")
     n = max(1, out[0])
-    return {"slices": out[0], "wait_us": out[1] / n / 100.0, "work_us": out[2] / n / 100.0}
+    return {"slices": out[0], "wait_us": out[1] / n / 100.0, "work_us": out[2] / n / 100.0,
+            "drain_us": out[3] / n / 100.0}
 
 
 def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:

@@ -37,7 +37,7 @@ static void group_discard() {
 
 static void fill_defaults(mccsCommConfig* c) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
-  if (c->block_threads <= 0) c->block_threads = 512;
+  if (c->block_threads <= 0) c->block_threads = MCCS_RING_MAX_THREADS;
   if (c->work_fifo_depth <= 0) c->work_fifo_depth = 4096;
   // launch on the caller's stream (stream order is the same as libmccs's
   // user-event -> comm-stream -> backend-event bridge, without the ~10 us per
@@ -49,8 +49,10 @@ static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
   // a chunk (buffer_size/2 bytes) must be a multiple of the largest thread
   // granule (512 x 8 B, all_reduce.h:34-35) so a rounded chunk fits 4 steps
   if (c.buffer_size < 8192 || c.buffer_size % 8192 != 0) return mccsInvalidArgument;
-  // multiples of 32 keep the reference's nWarps*32 blocks (e.g. 544) valid
-  if (c.block_threads < 64 || c.block_threads > MCCS_RING_MAX_THREADS || c.block_threads % 32) return mccsInvalidArgument;
+  // multiples of 32 keep the reference's nWarps*32 blocks (e.g. 544) valid;
+  // at least one data wave next to the control wave (ring_kernel.h), like
+  // the reference's smallest block (96 threads, plan.rs:602-635)
+  if (c.block_threads < 96 || c.block_threads > MCCS_RING_MAX_THREADS || c.block_threads % 32) return mccsInvalidArgument;
   if (c.lanes < 0 || c.lanes > MCCS_MAX_LANES) return mccsInvalidArgument;
   if (c.channel_count < 0 || c.channel_count > MCCS_MAX_NCHANNELS) return mccsInvalidArgument;
   if (c.work_fifo_depth & (c.work_fifo_depth - 1)) return mccsInvalidArgument;
@@ -161,7 +163,8 @@ using namespace mccs;
 extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   std::memset(cfg, 0, sizeof(*cfg));
   cfg->buffer_size = 1 << 22;
-  cfg->block_threads = 512;
+  // 8 data waves + the control wave (ring_kernel.h workgroup roles)
+  cfg->block_threads = MCCS_RING_MAX_THREADS;
   // FIFO data lives with the receiver: the sender's stores cross xGMI as
   // posted writes and every read is local HBM (the reference SHM default was
   // Sender for host-pinned memory; both remain selectable)

@@ -1,588 +1,54 @@
-// ring.hip — ring AllReduce / AllGather kernels for gfx950 (the mCCS device path).
-//
-// Drop-in for the reference kernels generated by src/collectives/src/common.h:
-// 182-188 (IMPL_COLL_KERN) with the same symbol names and signature
-//   extern "C" __global__ void mccsKernel_<Func>_RING_SIMPLE_<Op>_<T>(
-//       mccsDevComm* comm, uint64_t channelMask, mccsDevWork* workHead)
-// launched by the host as grid = (#channels in channelMask) x lanes,
-// block = any size (the reference host sends 96..544).
-//
-// Semantics restated (not translated) from the reference:
-//   kernel entry / work list ..... common.h:92-179 (blockIdx -> n-th set bit of
-//                                  channelMask; linked mccsDevWork list via
-//                                  workNext; isLast && inFifo -> *workFifoDone =
-//                                  doneAcks; abortFlag)
-//   AllReduce schedule ........... all_reduce.h:10-87 (chunk/loop sizes,
-//                                  realChunkSize rounding, 2(n-1) primitive calls)
-//   AllGather schedule ........... all_gather.h:7-79 (byte counts, userRanks)
-//   FIFO protocol ................ prims_simple.h:68-237 (8 slots, slice = 2
-//                                  steps, sender waits head+8 >= step+2,
-//                                  receiver waits tail >= step+2, post step+2)
-//   operand order ................ prims_simple.h:174-177 (srcs = [input, recv])
-//
-// What is MI355X-specific:
-//   * 64-lane waves; no 32-lane warp roles or named barriers.  One lane polls,
-//     the workgroup barrier publishes, every lane streams, every wave drains
-//     its stores (s_waitcnt vmcnt(0)) before one lane posts the step.
-//   * Lanes: a channel may be served by L workgroups (grid = nch * L), each
-//     owning a fixed 256-byte-aligned sub-range of every slice and its own
-//     head/tail flag line (ring_cfg.h), so more CUs stream one ring without
-//     any intra-channel synchronisation.  L = 1 is the reference layout.
-//   * FIFOs live in device memory over xGMI (host code: csrc/host/comm.cpp);
-//     flags are system-scope atomics; with uncached FIFO memory only vmcnt
-//     drains are needed, otherwise system-scope release/acquire fences.
-//   * Every spin is bounded: abortFlag is honoured and a watchdog (device
-//     timeout in the launch's mccsRingKernelCfg) raises abortFlag and an error bit.
-#include <hip/hip_runtime.h>
-
-#include "dtypes.h"
-#include "mccs_devcomm.h"
-#include "mccs_hip.h"
-#include "reduce_copy.h"
-#include "ring_cfg.h"
-
-// Cache policies of the slice streams (reduce_copy.h Policy), chosen by A/B
-// on the virtual node (tools/build_variant.sh + tools/ab_ring.sh, DESIGN.md
-// §3.2): the user input is read with nt loads (each element once per step)
-// and the user output written with nt stores: +3 / +10 / +13 % algbw at
-// n = 2 / 4 / 8 over plain accesses.  FIFO slots keep plain stores: the flag
-// protocol relies on a drained plain store having reached the FIFO memory.
-// Write-through (sc1) FIFO stores were faster still on one GPU but broke the
-// cross-process hand-off (tests/test_gpu_ipc.py: stale slot bytes seen after
-// the flag), and nt FIFO stores were 6-14 % slower.
-#ifndef MCCS_RING_INPUT_NT
-#define MCCS_RING_INPUT_NT 1
-#endif
-#ifndef MCCS_RING_OUT_POLICY
-#define MCCS_RING_OUT_POLICY kNonTemporal
-#endif
-#ifndef MCCS_RING_FIFO_POLICY
-#define MCCS_RING_FIFO_POLICY kPlain
-#endif
-
-namespace mccs {
-
-// Hand-off policy of the reference-named kernels (external planner: FIFO
-// memory of unknown kind, reference slicing).  Never written by the library.
-__device__ const mccsRingKernelCfg g_ref_cfg = {MCCS_FENCE_SYSTEM, ALLREDUCE_SLICESTEPS, 3000000000ull, 0, 0};  // 30 s
-__device__ unsigned long long g_ring_prof[MCCS_PROF_N];
-__device__ unsigned int g_ring_error = 0;
-
-constexpr int kSlots = MCCS_BUFFER_SLOTS;
-constexpr int kStepPerSlice = ALLREDUCE_SLICESTEPS;                           // 2
-constexpr int kChunkSteps = ALLREDUCE_CHUNKSTEPS;                             // 4
-constexpr int kLaneAlignBytes = 256;
-// 16-byte packs in flight per source per lane: a 64 KiB lane slice at 512
-// threads is one pass.  Byte types unpack 16 lanes per pack, so they use 4 to
-// stay within the register budget (no scratch).
-#ifndef MCCS_RING_UNROLL
-#define MCCS_RING_UNROLL 8
-#endif
-template <int DT>
-constexpr int kUnroll = kElemBytes<DT> == 1 ? (MCCS_RING_UNROLL < 4 ? MCCS_RING_UNROLL : 4) : MCCS_RING_UNROLL;
-
-struct RingShm {
-  mccsDevComm comm;
-  int pad0[2];
-  mccsDevChannel channel;
-  mccsDevWork work;
-  int aborted;
-};
-
-__device__ __forceinline__ uint64_t ld_flag(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_flag(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ bool abort_raised(volatile uint32_t* abortFlag) {
-  return abortFlag && __hip_atomic_load((uint32_t*)abortFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Poll load.  Uncached (fine-grained) flag lines are never held by an L2, so
-// a relaxed system-scope load sees the peer's store.  In a cached arena the
-// line may sit non-coherently in this XCD's L2, so every poll is an acquire
-// load (the load plus an L1/L2 invalidate): slower, but it cannot spin on a
-// stale copy forever (MI355X guide: "polling with ACQUIRE loads -> correct").
-__device__ __forceinline__ uint64_t ld_poll(const uint64_t* p, bool uncached) {
-  if (uncached) return ld_flag(p);
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// One lane of one wave polls; bounded by abortFlag and the watchdog.  *seen
-// keeps the last value read (flags only grow), so a later wait whose target it
-// already covers needs no memory round trip.
-__device__ __forceinline__ bool wait_geq(const uint64_t* flag, uint64_t target, volatile uint32_t* abortFlag, bool uncached,
-                         uint64_t* seen, uint64_t limit) {
-  if (*seen >= target) return true;
-  if ((*seen = ld_poll(flag, uncached)) >= target) return true;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t spins = 0;
-  while ((*seen = ld_poll(flag, uncached)) < target) {
-    if (++spins >= 64) {
-      spins = 0;
-      if (abort_raised(abortFlag)) {
-        atomicOr(&g_ring_error, MCCS_ERR_ABORTED);
-        return false;
-      }
-      if (limit && __builtin_amdgcn_s_memrealtime() - t0 > limit) {
-        atomicOr(&g_ring_error, MCCS_ERR_TIMEOUT);
-        if (abortFlag)
-          __hip_atomic_store((uint32_t*)abortFlag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return false;
-      }
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return true;
-}
-
-// Per-workgroup view of one channel lane's two connectors (prims_simple.h roles,
-// collapsed: lane 0 of thread 0 waits and posts for the whole workgroup).
-template <int DT, int OP>
-struct RingPrims {
-  using T = typename Elem<DT>::T;
-  int tid, nthr, lane, nlanes;
-  int64_t stepSize;  // elements per FIFO step
-  const T* input;
-  T* output;
-  // recv side: data from prev
-  const T* rbuf;
-  uint64_t* r_wait;  // local tail line (we poll)
-  uint64_t* r_post;  // remote head line (we post)
-  uint64_t r_step;
-  // send side: data to next
-  T* sbuf;
-  uint64_t* s_wait;  // local head line (we poll)
-  uint64_t* s_post;  // remote tail line (we post)
-  uint64_t s_step;
-  uint64_t r_seen, s_seen;  // thread 0: last tail / head values read
-  int sps, spc;              // FIFO steps per slice, slices per chunk (sps * spc = ALLREDUCE_CHUNKSTEPS)
-  bool prof;                 // accumulate g_ring_prof
-  uint64_t prof_n, prof_wait, prof_work;  // thread 0: this work element's slice timing
-  volatile uint32_t* abortFlag;
-  uint64_t timeout;          // watchdog, s_memrealtime ticks (0 = never)
-  bool uncached;
-  int* aborted;  // LDS
-
-  template <int RECV, int SEND, int SRC, int DST>
-  __device__ __forceinline__ void op(int64_t srcIx, int64_t dstIx, int64_t nelem) {
-    constexpr int64_t kAlign = kLaneAlignBytes / (int64_t)sizeof(T);
-    if (*aborted) return;  // uniform: last written before a barrier
-    if (nelem < 0) nelem = 0;
-    int64_t sliceSize = stepSize * sps;
-    {
-      int64_t s = (nelem + 16 * spc - 1) / (16 * spc) * 16;
-      sliceSize = s > sliceSize / 32 ? s : sliceSize / 32;  // prims_simple.h:156-157
-    }
-    int64_t offset = 0;
-#pragma unroll 1
-    for (int slice = 0; slice < spc; ++slice) {
-      int64_t real = nelem - offset;
-      real = real < sliceSize ? real : sliceSize;
-      if (real < 0) real = 0;
-      // Lane partition.  Each lane owns a FIXED region of every 2-step slot
-      // pair (laneCap elements, the last lane the rest), independent of this
-      // slice's size: lanes run ahead of each other by up to 4 slices, so a
-      // size-dependent split would let lane k overwrite FIFO bytes lane k+1's
-      // receiver has not consumed yet.  Lane 0 region starts at the slot, so a
-      // single lane reproduces the reference FIFO layout exactly.
-      const int64_t span = stepSize * sps;
-      const int64_t laneCap = span / nlanes / kAlign * kAlign;
-      int64_t part = (real + nlanes - 1) / nlanes;
-      part = (part + kAlign - 1) / kAlign * kAlign;
-      part = part < laneCap ? part : laneCap;
-      int64_t lo = (int64_t)lane * part;
-      lo = lo < real ? lo : real;
-      int64_t hi = (lane == nlanes - 1) ? real : (lo + part < real ? lo + part : real);
-      const int64_t fifoOff = (int64_t)lane * laneCap;  // this lane's region in the slot pair
-      uint64_t t_start = 0, t_ready = 0;
-      if (tid == 0 && prof) t_start = __builtin_amdgcn_s_memrealtime();
-      if (tid == 0) {
-        bool ok = true;
-        if (RECV) ok = wait_geq(r_wait, r_step + sps, abortFlag, uncached, &r_seen, timeout);
-        if (ok && SEND) {
-          const uint64_t need = s_step + sps;
-          ok = wait_geq(s_wait, need > (uint64_t)kSlots ? need - kSlots : 0, abortFlag, uncached, &s_seen, timeout);
-        }
-        if (!ok) *aborted = 1;
-        if (prof) t_ready = __builtin_amdgcn_s_memrealtime();
-        if (ok && RECV && !uncached) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      if (*aborted) return;
-      if (hi > lo) {
-        // operands in ReduceOrCopyMulti order: src0 = own input (SRC) else the
-        // receive slot; src1 = the receive slot when both (prims_simple.h:174-177)
-        constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
-        constexpr int ND = (DST ? 1 : 0) + (SEND ? 1 : 0);
-        const T* rslot = rbuf + (int64_t)(r_step % kSlots) * stepSize + fifoOff;
-        T* sslot = sbuf + (int64_t)(s_step % kSlots) * stepSize + fifoOff;
-        const T* s0 = SRC ? input + srcIx + offset + lo : rslot;
-        T* d0 = DST ? output + dstIx + offset + lo : sslot;
-        // the receive slot is rewritten by the peer between our reads of it:
-        // read it with non-temporal loads so no stale copy in this CU's L1 is
-        // ever hit (a plain re-read of an L1-resident FIFO line returns the
-        // previous step's bytes; MI355X guide, inter-workgroup visibility)
-        constexpr int kRecvNt = RECV ? (SRC ? 2 : 1) : 0;
-        constexpr int kInNt = (SRC && MCCS_RING_INPUT_NT) ? 1 : 0;  // user input: read once per step
-        constexpr int kD0 = DST ? MCCS_RING_OUT_POLICY : MCCS_RING_FIFO_POLICY;
-        reduce_copy_rows<DT, OP, kUnroll<DT>, NS, ND, kRecvNt | kInNt, kD0, MCCS_RING_FIFO_POLICY>(
-            s0, rslot, d0, sslot, hi - lo, tid, nthr);
-      }
-      // Thread 0 reads the flags the next slice waits on now, so their latency
-      // hides under the drain (a value that already covers the next target
-      // saves that wait's round trip).  Reading is all it does: the post
-      // below never waits on the next slice (deferring it could deadlock).
-      uint64_t r_pre = 0, s_pre = 0;
-      if (tid == 0) {
-        if (RECV) r_pre = ld_poll(r_wait, uncached);
-        if (SEND) s_pre = ld_poll(s_wait, uncached);
-      }
-      // every wave drains its FIFO stores and loads before the step is posted
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        r_seen = r_pre > r_seen ? r_pre : r_seen;
-        s_seen = s_pre > s_seen ? s_pre : s_seen;
-        if (prof) {  // summed in registers; flushed once per work element (save_steps)
-          const uint64_t t_done = __builtin_amdgcn_s_memrealtime();
-          prof_n += 1;
-          prof_wait += t_ready - t_start;
-          prof_work += t_done - t_ready;
-        }
-        if (SEND) {
-          if (!uncached) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see MI355X guide: compiler hazard
-          }
-          st_flag(s_post, s_step + sps);
-        }
-        if (RECV) st_flag(r_post, r_step + sps);
-      }
-      if (RECV) r_step += sps;
-      if (SEND) s_step += sps;
-      offset += sliceSize;
-    }
-  }
-  // prims_simple.h:557-611 entry points used by the ring schedules
-  __device__ void send(int64_t inIx, int64_t n) { op<0, 1, 1, 0>(inIx, 0, n); }
-  __device__ void copySend(int64_t inIx, int64_t outIx, int64_t n) { op<0, 1, 1, 1>(inIx, outIx, n); }
-  __device__ void recvReduceSend(int64_t inIx, int64_t n) { op<1, 1, 1, 0>(inIx, 0, n); }
-  __device__ void recvReduceCopySend(int64_t inIx, int64_t outIx, int64_t n) { op<1, 1, 1, 1>(inIx, outIx, n); }
-  __device__ void recvCopySend(int64_t outIx, int64_t n) { op<1, 1, 0, 1>(0, outIx, n); }
-  __device__ void recv(int64_t outIx, int64_t n) { op<1, 0, 0, 1>(0, outIx, n); }
-};
-
-__device__ __forceinline__ int64_t div_up(int64_t a, int64_t b) { return (a + b - 1) / b; }
-__device__ __forceinline__ int64_t round_up(int64_t a, int64_t b) { return div_up(a, b) * b; }
-
-// Sets up a lane's connectors from channel.peers (the reference's
-// loadRecvConn/loadSendConn, prims_simple.h:315-398).  Steps come from the
-// lane's own flag line (word 1); lane 0 mirrors them into conn->step.
-template <int DT, int OP>
-__device__ __forceinline__ void setup_prims(RingPrims<DT, OP>& p, RingShm& shm, const mccsDevWorkElem& e, int lane,
-                            int nlanes, const mccsRingKernelCfg& cfg) {
-  using T = typename Elem<DT>::T;
-  const mccsDevRing& ring = shm.channel.ring;
-  mccsDevConnInfo* rc = &shm.channel.peers[ring.prev].recv[0];
-  mccsDevConnInfo* sc = &shm.channel.peers[ring.next].send[0];
-  p.tid = threadIdx.x;
-  p.nthr = blockDim.x;
-  p.lane = lane;
-  p.nlanes = nlanes;
-  p.stepSize = shm.comm.buffSizes[MCCS_PROTO_SIMPLE] / kSlots / (int)sizeof(T);
-  p.input = (const T*)e.sendbuff;
-  p.output = (T*)e.recvbuff;
-  p.rbuf = (const T*)rc->buffs[MCCS_PROTO_SIMPLE];
-  p.r_wait = rc->tail + lane * MCCS_FLAG_LINE_WORDS;
-  p.r_post = rc->head + lane * MCCS_FLAG_LINE_WORDS;
-  p.sbuf = (T*)sc->buffs[MCCS_PROTO_SIMPLE];
-  p.s_wait = sc->head + lane * MCCS_FLAG_LINE_WORDS;
-  p.s_post = sc->tail + lane * MCCS_FLAG_LINE_WORDS;
-  p.r_step = ld_flag(p.r_wait + 1);
-  p.s_step = ld_flag(p.s_wait + 1);
-  // Primitives ctor rounds to SlicePerChunk*StepPerSlice (prims_simple.h:318-319)
-  p.r_step = (p.r_step + 3) / 4 * 4;
-  p.s_step = (p.s_step + 3) / 4 * 4;
-  p.r_seen = 0;
-  p.s_seen = 0;
-  p.sps = cfg.slice_steps == kChunkSteps ? kChunkSteps : kStepPerSlice;
-  p.spc = kChunkSteps / p.sps;
-  p.prof = cfg.profile != 0;
-  p.timeout = cfg.timeout_ticks;
-  p.prof_n = p.prof_wait = p.prof_work = 0;
-  p.abortFlag = shm.comm.abortFlag;
-  p.uncached = cfg.fence_mode == MCCS_FENCE_UNCACHED;
-  p.aborted = &shm.aborted;
-}
-
-template <int DT, int OP>
-__device__ __forceinline__ void save_steps(RingPrims<DT, OP>& p, RingShm& shm) {
-  __syncthreads();
-  if (p.tid == 0) {
-    if (p.prof && p.prof_n) {
-      atomicAdd(&g_ring_prof[MCCS_PROF_SLICES], (unsigned long long)p.prof_n);
-      atomicAdd(&g_ring_prof[MCCS_PROF_WAIT], (unsigned long long)p.prof_wait);
-      atomicAdd(&g_ring_prof[MCCS_PROF_WORK], (unsigned long long)p.prof_work);
-    }
-    st_flag(p.r_wait + 1, p.r_step);
-    st_flag(p.s_wait + 1, p.s_step);
-    if (p.lane == 0) {  // reference-visible copy (prims_simple.h:454-466)
-      const mccsDevRing& ring = shm.channel.ring;
-      shm.channel.peers[ring.prev].recv[0].step = p.r_step;
-      shm.channel.peers[ring.next].send[0].step = p.s_step;
-    }
-  }
-  __syncthreads();
-}
-
-// n == 1: no connectors exist (reference transport/setup.rs:411 loops 1..n);
-// defined here as the identity (recvbuff = sendbuff).
-template <int DT>
-__device__ __forceinline__ void local_copy(const mccsDevWorkElem& e, int block_in_ch, int nblocks_ch) {
-  using T = typename Elem<DT>::T;
-  if (e.sendbuff == e.recvbuff) return;
-  const int64_t per = div_up((int64_t)e.count, (int64_t)e.nChannels);
-  const int64_t lo0 = (int64_t)e.bid * per;
-  const int64_t hi0 = lo0 + per < (int64_t)e.count ? lo0 + per : (int64_t)e.count;
-  if (hi0 <= lo0) return;
-  const int64_t span = hi0 - lo0;
-  const int64_t part = round_up(div_up(span, nblocks_ch), 64);
-  const int64_t lo = lo0 + (int64_t)block_in_ch * part;
-  const int64_t hi = lo + part < hi0 ? lo + part : hi0;
-  if (hi <= lo) return;
-  reduce_copy_rows<DT, OpSum, kUnroll<DT>, 1, 1, 0>((const T*)e.sendbuff + lo, nullptr, (T*)e.recvbuff + lo, nullptr,
-                                               hi - lo, threadIdx.x, blockDim.x);
-}
-
-// all_reduce.h:10-87
-template <int DT, int OP>
-__device__ __forceinline__ void run_allreduce(RingShm& shm, const mccsDevWorkElem& e, int lane, int nlanes,
-                                              const mccsRingKernelCfg& cfg) {
-  using T = typename Elem<DT>::T;
-  const int nranks = shm.comm.nRanks;
-  if (nranks == 1) {
-    local_copy<DT>(e, lane, nlanes);
-    return;
-  }
-  RingPrims<DT, OP> p;
-  setup_prims(p, shm, e, lane, nlanes, cfg);
-  const int ringIx = shm.channel.ring.index;
-  const int64_t chunkSize = (int64_t)(int)(p.stepSize * ALLREDUCE_CHUNKSTEPS);
-  const int64_t loopSize = (int64_t)e.nChannels * nranks * chunkSize;
-  const int64_t size = (int64_t)e.count;
-  const int nthreads_ref = (int)e.nWarps * WARP_SIZE;
-  int64_t gran = (int64_t)(nthreads_ref - WARP_SIZE) * 8 / (int64_t)sizeof(T);
-  if (gran < 1) gran = 1;
-  auto modRanks = [&](int r) { return r >= nranks ? r - nranks : r; };
-#pragma unroll 1
-  for (int64_t gridOffset = 0; gridOffset < size; gridOffset += loopSize) {
-    int64_t rcs = div_up(size - gridOffset, (int64_t)e.nChannels * nranks);
-    rcs = chunkSize < rcs ? chunkSize : rcs;
-    rcs = (int64_t)(int)round_up(rcs, gran);
-    auto calcOffset = [&](int chunk) { return gridOffset + (int64_t)e.bid * nranks * rcs + (int64_t)chunk * rcs; };
-    auto nel = [&](int64_t off) { return rcs < size - off ? rcs : size - off; };
-    int chunk = modRanks(ringIx + nranks - 1);
-    int64_t off = calcOffset(chunk);
-    p.send(off, nel(off));
-    for (int j = 2; j < nranks; ++j) {
-      chunk = modRanks(ringIx + nranks - j);
-      off = calcOffset(chunk);
-      p.recvReduceSend(off, nel(off));
-    }
-    chunk = ringIx;
-    off = calcOffset(chunk);
-    p.recvReduceCopySend(off, off, nel(off));
-    for (int j = 1; j < nranks - 1; ++j) {
-      chunk = modRanks(ringIx + nranks - j);
-      off = calcOffset(chunk);
-      p.recvCopySend(off, nel(off));
-    }
-    chunk = modRanks(ringIx + 1);
-    off = calcOffset(chunk);
-    p.recv(off, nel(off));
-    if (shm.aborted) break;
-  }
-  save_steps(p, shm);
-}
-
-// all_gather.h:7-79 (int8 kernel: count is bytes)
-__device__ __forceinline__ void run_allgather(RingShm& shm, const mccsDevWorkElem& e, int lane, int nlanes,
-                                              const mccsRingKernelCfg& cfg) {
-  constexpr int DT = mccsInt8;
-  const int nranks = shm.comm.nRanks;
-  const int64_t size = (int64_t)e.count;
-  if (nranks == 1) {
-    local_copy<DT>(e, lane, nlanes);
-    return;
-  }
-  RingPrims<DT, OpSum> p;
-  setup_prims(p, shm, e, lane, nlanes, cfg);
-  const int* ringRanks = shm.channel.ring.userRanks;
-  const int64_t chunkSize = (int64_t)(int)(p.stepSize * ALLGATHER_CHUNKSTEPS);
-  const int64_t loopSize = (int64_t)e.nChannels * chunkSize;
-  const int nthreads_ref = (int)e.nWarps * WARP_SIZE;
-  int64_t gran = (int64_t)(nthreads_ref - WARP_SIZE) * 8;
-  if (gran < 1) gran = 1;
-#pragma unroll 1
-  for (int64_t gridOffset = 0; gridOffset < size; gridOffset += loopSize) {
-    int64_t rcs = div_up(size - gridOffset, (int64_t)e.nChannels);
-    rcs = chunkSize < rcs ? chunkSize : rcs;
-    rcs = (int64_t)(int)round_up(rcs, gran);
-    const int64_t chunkOffset = gridOffset + (int64_t)(int)(e.bid * rcs);
-    const int64_t nelem = rcs < size - chunkOffset ? rcs : size - chunkOffset;
-    int rankDest = ringRanks[0];
-    int64_t offset = chunkOffset + (int64_t)rankDest * size;
-    if ((const char*)e.sendbuff + chunkOffset == (const char*)e.recvbuff + offset)
-      p.send(chunkOffset, nelem);  // in place: directSend
-    else
-      p.copySend(chunkOffset, offset, nelem);  // directCopySend
-    for (int j = 1; j < nranks - 1; ++j) {
-      rankDest = ringRanks[nranks - j];
-      offset = chunkOffset + (int64_t)rankDest * size;
-      p.recvCopySend(offset, nelem);
-    }
-    rankDest = ringRanks[1];
-    offset = chunkOffset + (int64_t)rankDest * size;
-    p.recv(offset, nelem);
-    if (shm.aborted) break;
-  }
-  save_steps(p, shm);
-}
-
-__device__ __forceinline__ void copy_words(void* dst, const void* src, int bytes) {
-  for (int i = threadIdx.x * 4; i < bytes; i += blockDim.x * 4)
-    *(uint32_t*)((char*)dst + i) = *(const uint32_t*)((const char*)src + i);
-}
-
-// common.h:92-179 restated for gfx950.  `block`/`nblocks` are this rank's
-// workgroup index and count (blockIdx.x / gridDim.x for a normal launch).
-template <int FN, int DT, int OP>
-__device__ __forceinline__ void ring_kernel_body(mccsDevComm* comm, uint64_t channelMask, mccsDevWork* workHead, int block,
-                                 int nblocks, const mccsRingKernelCfg& cfg) {
-  __shared__ RingShm shm;
-  const int nch = __popcll(channelMask);
-  if (nch == 0) return;
-  const int nlanes = nblocks / nch > 0 ? nblocks / nch : 1;
-  const int chIdx = block / nlanes;
-  const int lane = block % nlanes;
-  if (chIdx >= nch) return;  // surplus workgroups
-  // chIdx-th set bit of channelMask -> channel id
-  int channelId = 0;
-  {
-    uint64_t m = channelMask;
-    for (int i = 0; i < chIdx; ++i) m &= m - 1;
-    channelId = __ffsll((unsigned long long)m) - 1;
-  }
-  copy_words(&shm.comm, comm, sizeof(mccsDevComm));
-  copy_words(&shm.channel, &((mccsDevCommAndChannels*)comm)->channels[channelId], sizeof(mccsDevChannel));
-  copy_words(&shm.work, workHead + chIdx, sizeof(mccsDevWork));
-  if (threadIdx.x == 0) shm.aborted = 0;
-  __syncthreads();
-#pragma unroll 1
-  while (true) {
-    if (threadIdx.x == 0 && lane == 0 && shm.work.header.isLast && shm.work.header.inFifo)
-      __hip_atomic_store(shm.channel.workFifoDone, shm.work.header.doneAcks, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
-    for (int i = 0; i < MCCS_MAX_WORK_ELEMENTS; ++i) {
-      const mccsDevWorkElem& e = shm.work.elems[i];
-      if (!e.isUsed) break;
-      if constexpr (FN == mccsFuncAllReduce) run_allreduce<DT, OP>(shm, e, lane, nlanes, cfg);
-      else run_allgather(shm, e, lane, nlanes, cfg);
-      __syncthreads();
-      if (shm.aborted) break;
-    }
-    const int32_t next = shm.work.header.workNext;
-    const bool last = shm.work.header.isLast;
-    __syncthreads();
-    if (last || shm.aborted) break;
-    copy_words(&shm.work, workHead + next, sizeof(mccsDevWork));
-    __syncthreads();
-    if (abort_raised(shm.comm.abortFlag)) break;
-  }
-}
-
-// Multi-rank launch: blockIdx.y selects the communicator (ranks sharing a GPU).
-template <int FN, int DT, int OP>
-__global__ void __launch_bounds__(MCCS_RING_MAX_THREADS) ring_multi_kernel(mccsMultiLaunchArgs a) {
-  ring_kernel_body<FN, DT, OP>(a.comm[blockIdx.y], a.channelMask, a.work[blockIdx.y], blockIdx.x, gridDim.x, a.cfg);
-}
-
-}  // namespace mccs
-
-using namespace mccs;
-
-// ---- reference-named kernels (symbol-level swap for collectives-sys) -------
-#define MCCS_AR_KERNEL(OPN, OPV, TN, DT)                                                             \
-  extern "C" __global__ void __launch_bounds__(MCCS_RING_MAX_THREADS)                                                \
-      mccsKernel_AllReduce_RING_SIMPLE_##OPN##_##TN(mccsDevComm* comm, uint64_t channelMask,        \
-                                                    mccsDevWork* workHead) {                         \
-    ring_kernel_body<mccsFuncAllReduce, DT, OPV>(comm, channelMask, workHead, blockIdx.x, gridDim.x, g_ref_cfg); \
-  }
-#define MCCS_AR_KERNELS_FOR_OP(OPN, OPV)                  \
-  MCCS_AR_KERNEL(OPN, OPV, int8_t, mccsInt8)              \
-  MCCS_AR_KERNEL(OPN, OPV, uint8_t, mccsUint8)            \
-  MCCS_AR_KERNEL(OPN, OPV, int32_t, mccsInt32)            \
-  MCCS_AR_KERNEL(OPN, OPV, uint32_t, mccsUint32)          \
-  MCCS_AR_KERNEL(OPN, OPV, int64_t, mccsInt64)            \
-  MCCS_AR_KERNEL(OPN, OPV, uint64_t, mccsUint64)          \
-  MCCS_AR_KERNEL(OPN, OPV, half, mccsFloat16)             \
-  MCCS_AR_KERNEL(OPN, OPV, float, mccsFloat32)            \
-  MCCS_AR_KERNEL(OPN, OPV, double, mccsFloat64)           \
-  MCCS_AR_KERNEL(OPN, OPV, bfloat16, mccsBfloat16)
-
-MCCS_AR_KERNELS_FOR_OP(Sum, OpSum)
-MCCS_AR_KERNELS_FOR_OP(Prod, OpProd)
-MCCS_AR_KERNELS_FOR_OP(Max, OpMax)
-MCCS_AR_KERNELS_FOR_OP(Min, OpMin)
+// ring.hip — AllGather ring kernel, kernel tables and device-wide helpers of
+// the ring path.  The device engine is ring_kernel.h; the forty AllReduce
+// kernels live in ring_ar_{sum,prod,max,min}.hip (one translation unit per
+// reduction op, compiled in parallel).
+#include "ring_kernel.h"
 
 extern "C" __global__ void __launch_bounds__(MCCS_RING_MAX_THREADS)
     mccsKernel_AllGather_RING_SIMPLE_Sum_int8_t(mccsDevComm* comm, uint64_t channelMask, mccsDevWork* workHead) {
-  ring_kernel_body<mccsFuncAllGather, mccsInt8, OpSum>(comm, channelMask, workHead, blockIdx.x, gridDim.x, g_ref_cfg);
+  mccs::ring_kernel_body<mccsFuncAllGather, mccsInt8, mccs::OpSum>(comm, channelMask, workHead, blockIdx.x,
+                                                                    gridDim.x, mccs::kRefCfg);
 }
+
+MCCS_RING_TU_ACCESSORS(ag)
 
 // ---- host-side kernel tables ------------------------------------------------
 namespace mccs {
 
-#define MCCS_KP(OPN, TN) (const void*)&mccsKernel_AllReduce_RING_SIMPLE_##OPN##_##TN
-#define MCCS_KROW(OPN)                                                                            \
-  {MCCS_KP(OPN, int8_t), MCCS_KP(OPN, uint8_t), MCCS_KP(OPN, int32_t), MCCS_KP(OPN, uint32_t),    \
-   MCCS_KP(OPN, int64_t), MCCS_KP(OPN, uint64_t), MCCS_KP(OPN, half), MCCS_KP(OPN, float),         \
-   MCCS_KP(OPN, double), MCCS_KP(OPN, bfloat16)}
-static const void* const kAllReduceKernels[4][mccsNumTypes] = {MCCS_KROW(Sum), MCCS_KROW(Prod),
-                                                               MCCS_KROW(Max), MCCS_KROW(Min)};
+const void* ring_ar_kernel_Sum(int dtype, bool multi);
+const void* ring_ar_kernel_Prod(int dtype, bool multi);
+const void* ring_ar_kernel_Max(int dtype, bool multi);
+const void* ring_ar_kernel_Min(int dtype, bool multi);
+hipError_t ring_tu_ar_sum_read_profile(unsigned long long* out, bool reset);
+hipError_t ring_tu_ar_prod_read_profile(unsigned long long* out, bool reset);
+hipError_t ring_tu_ar_max_read_profile(unsigned long long* out, bool reset);
+hipError_t ring_tu_ar_min_read_profile(unsigned long long* out, bool reset);
+hipError_t ring_tu_ar_sum_take_error(unsigned* err);
+hipError_t ring_tu_ar_prod_take_error(unsigned* err);
+hipError_t ring_tu_ar_max_take_error(unsigned* err);
+hipError_t ring_tu_ar_min_take_error(unsigned* err);
 
-template <int FN, int DT>
-static const void* multi_ptr(int op) {
+static const void* ar_kernel(int dtype, int op, bool multi) {
+  if (dtype < 0 || dtype >= mccsNumTypes) return nullptr;
   switch (op) {
-    case OpSum: return (const void*)&ring_multi_kernel<FN, DT, OpSum>;
-    case OpProd: return (const void*)&ring_multi_kernel<FN, DT, OpProd>;
-    case OpMax: return (const void*)&ring_multi_kernel<FN, DT, OpMax>;
-    case OpMin: return (const void*)&ring_multi_kernel<FN, DT, OpMin>;
+    case OpSum: return ring_ar_kernel_Sum(dtype, multi);
+    case OpProd: return ring_ar_kernel_Prod(dtype, multi);
+    case OpMax: return ring_ar_kernel_Max(dtype, multi);
+    case OpMin: return ring_ar_kernel_Min(dtype, multi);
   }
   return nullptr;
 }
 
 const void* ring_kernel_ptr(int func, int dtype, int op) {
   if (func == mccsFuncAllGather) return (const void*)&mccsKernel_AllGather_RING_SIMPLE_Sum_int8_t;
-  if (func != mccsFuncAllReduce || dtype < 0 || dtype >= mccsNumTypes || op < 0 || op > OpMin) return nullptr;
-  return kAllReduceKernels[op][dtype];
+  if (func != mccsFuncAllReduce) return nullptr;
+  return ar_kernel(dtype, op, false);
 }
 
 const void* ring_multi_kernel_ptr(int func, int dtype, int op) {
   if (func == mccsFuncAllGather) return (const void*)&ring_multi_kernel<mccsFuncAllGather, mccsInt8, OpSum>;
   if (func != mccsFuncAllReduce) return nullptr;
-  switch (dtype) {
-#define X(D) \
-  case D: return multi_ptr<mccsFuncAllReduce, D>(op);
-    MCCS_FOR_EACH_DTYPE(X)
-#undef X
-  }
-  return nullptr;
+  return ar_kernel(dtype, op, true);
 }
 
 // Writes back and invalidates every XCD's L2 and the CUs' L1 (system-scope
@@ -601,22 +67,31 @@ hipError_t ring_flush_caches(hipStream_t st) {
   return hipGetLastError();
 }
 
-// Reads (and optionally zeroes) the current device's ring profile counters.
+// Reads (and optionally zeroes) the current device's ring profile counters,
+// summed over the translation units that hold ring kernels.
 hipError_t ring_read_profile(unsigned long long* out, bool reset) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ring_prof), sizeof(g_ring_prof), 0, hipMemcpyDeviceToHost);
-  if (e == hipSuccess && reset) {
-    unsigned long long zero[MCCS_PROF_N] = {};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_ring_prof), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+  for (int i = 0; i < MCCS_PROF_N; ++i) out[i] = 0;
+  hipError_t (*const readers[])(unsigned long long*, bool) = {
+      ring_tu_ag_read_profile, ring_tu_ar_sum_read_profile, ring_tu_ar_prod_read_profile,
+      ring_tu_ar_max_read_profile, ring_tu_ar_min_read_profile};
+  for (auto rd : readers) {
+    hipError_t e = rd(out, reset);
+    if (e != hipSuccess) return e;
   }
-  return e;
+  return hipSuccess;
 }
 
+// ORs (and clears) the device error words of every ring translation unit.
 hipError_t ring_take_device_error(unsigned* err) {
-  unsigned zero = 0;
-  hipError_t e = hipMemcpyFromSymbol(err, HIP_SYMBOL(g_ring_error), sizeof(unsigned), 0, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return e;
-  if (*err) e = hipMemcpyToSymbol(HIP_SYMBOL(g_ring_error), &zero, sizeof(zero), 0, hipMemcpyHostToDevice);
-  return e;
+  *err = 0;
+  hipError_t (*const takers[])(unsigned*) = {ring_tu_ag_take_error, ring_tu_ar_sum_take_error,
+                                             ring_tu_ar_prod_take_error, ring_tu_ar_max_take_error,
+                                             ring_tu_ar_min_take_error};
+  for (auto tk : takers) {
+    hipError_t e = tk(err);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace mccs
@@ -629,7 +104,9 @@ extern "C" mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, mccsDe
                                              mccsDevWork* workHead, unsigned grid, unsigned block,
                                              hipStream_t stream) {
   const void* fn = mccs::ring_kernel_ptr(func, dtype, op);
-  if (!fn || !comm || !workHead || grid == 0 || block == 0 || block > MCCS_RING_MAX_THREADS) return mccsInvalidArgument;
+  // blocks of one wave have no control wave (ring_kernel.h); the reference
+  // host never launches fewer than 96 threads (get_task_schema, plan.rs:602-635)
+  if (!fn || !comm || !workHead || grid == 0 || block <= 64 || block > MCCS_RING_MAX_THREADS) return mccsInvalidArgument;
   void* args[3] = {&comm, &channelMask, &workHead};
   hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, stream);
   return e == hipSuccess ? mccsSuccess : mccsUnhandledCudaError;

@@ -44,6 +44,7 @@ struct mccsRingKernelCfg {
 #define MCCS_PROF_SLICES 0  // slices executed
 #define MCCS_PROF_WAIT 1    // slice start -> peer flags satisfied (thread 0)
 #define MCCS_PROF_WORK 2    // flags satisfied -> stores drained, both barriers included
+#define MCCS_PROF_DRAIN 3   // part of WORK: thread 0's wave done issuing -> every wave drained (barrier)
 #define MCCS_PROF_N 4
 
 // Communicator launch: one or several communicators of one device in ONE

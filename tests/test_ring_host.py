@@ -65,7 +65,7 @@ def test_config_struct_matches_header():
     lib = comm._sig()
     c = _CommConfig()
     lib.mccsCommConfigDefault(ctypes.byref(c))
-    assert c.buffer_size == 1 << 22 and c.block_threads == 512 and c.work_fifo_depth == 4096
+    assert c.buffer_size == 1 << 22 and c.block_threads == 576 and c.work_fifo_depth == 4096
     assert c.locality == comm.LOCALITY_RECEIVER and c.fifo_memory == comm.FIFO_UNCACHED
 
 

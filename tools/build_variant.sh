@@ -1,14 +1,20 @@
 #!/usr/bin/env bash
 # Builds an A/B variant of libmccs_hip.so with extra -D flags into exp/<name>.so
-# (use it with MCCS_LIB_PATH=exp/<name>.so).  Only ring.hip is recompiled.
+# (use it with MCCS_LIB_PATH=exp/<name>.so).  Only the ring translation units
+# (ring.hip, ring_ar_*.hip) are recompiled, in parallel.
 #   tools/build_variant.sh <name> -DMCCS_RING_INPUT_NT=1 ...
 set -eu
 R=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
 mkdir -p "$R/exp/$name"
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -I"$R/mccs_amd/csrc" "$@" \
-  -c -x hip "$R/mccs_amd/csrc/ring.hip" -o "$R/exp/$name/ring.o"
-objs=$(ls "$R"/build/obj/*.o | grep -v '/ring.hip.o$')
-hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/exp/$name.so" "$R/exp/$name/ring.o" $objs -lpthread
+pids=()
+for src in "$R"/mccs_amd/csrc/ring*.hip; do
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -I"$R/mccs_amd/csrc" "$@" \
+    -c -x hip "$src" -o "$R/exp/$name/$(basename "$src").o" &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait "$p"; done
+objs=$(ls "$R"/build/obj/*.o | grep -v '/ring[^/]*\.hip\.o$')
+hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/exp/$name.so" "$R"/exp/$name/*.o $objs -lpthread
 rm -rf "$R/exp/$name"
 echo "$R/exp/$name.so"

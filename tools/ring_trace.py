@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Slice timeline of the ring engine on a virtual node (one GPU).
+
+Needs a -DMCCS_RING_TRACE build:
+  tools/build_variant.sh trace -DMCCS_RING_TRACE
+  MCCS_LIB_PATH=exp/trace.so python tools/ring_trace.py --n 2 --lanes 16 --mib 128
+Prints, per rank slot and slice of lane 0 of channel 0 (s_memrealtime, 10 ns
+ticks, relative to the first event): when the control wave made the slice
+ready, when data waves started / finished issuing / drained, when it was
+posted, and the detection latency (our ready of t+1 - prev's post of t).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+EV = {1: "ready", 2: "start", 3: "issued", 4: "drained", 5: "added", 6: "post"}
+
+
+def main():
+    import torch
+
+    from mccs_amd import _lib
+    from mccs_amd import comm as C
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=2)
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--mib", type=int, default=128)
+    ap.add_argument("--show", type=int, default=12, help="slices printed per rank")
+    args = ap.parse_args()
+    lib = _lib.load()
+    fn = lib.mccs_ring_trace_ar_sum
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    fn.restype = ctypes.c_int
+    n = args.n
+    comms = C.init_all([0] * n, C.CommConfig(lanes=args.lanes))
+    cnt = (args.mib << 20) // 4
+    xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
+    ys = [torch.empty_like(x) for x in xs]
+
+    def once():
+        with C.group():
+            for r in range(n):
+                C.all_reduce(comms[r], xs[r], ys[r], cnt, C.AllReduceDataType.Float32)
+        for c in comms:
+            c.sync()
+        torch.cuda.synchronize()
+
+    once()
+    buf = (ctypes.c_ulonglong * (2 << 15))()
+    fn(buf, 1 << 15)  # clear
+    once()
+    k = fn(buf, 1 << 15)
+    ev = defaultdict(lambda: defaultdict(list))  # (rank) -> (t, ev) -> [(ts, wave)]
+    t0 = min(buf[2 * i] for i in range(k)) if k else 0
+    for i in range(k):
+        ts, w = buf[2 * i] - t0, buf[2 * i + 1]
+        e, wave, rank, t = w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFFFF, w >> 32
+        ev[rank][(t, EV[e])].append((ts, wave))
+    rings = comms[0].rings()
+    out = {"events": k, "n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels}
+    print(json.dumps(out))
+    nsl = max(t for r in ev for (t, _) in ev[r]) + 1 if k else 0
+    lat, per = [], []
+    for r in sorted(ev):
+        prev = rings[0][(rings[0].index(r) - 1) % n]
+        print(f"rank {r} (prev {prev})  t: ready start[min,max] issued[min,max] drained[max] post  | detect")
+        for t in range(nsl):
+            g = ev[r]
+            rd = min((x for x, _ in g.get((t, "ready"), [])), default=None)
+            st = [x for x, _ in g.get((t, "start"), [])]
+            iss = [x for x, _ in g.get((t, "issued"), [])]
+            dr = [x for x, _ in g.get((t, "drained"), [])]
+            po = min((x for x, _ in g.get((t, "post"), [])), default=None)
+            ppost = min((x for x, _ in ev[prev].get((t - 1, "post"), [])), default=None) if t else None
+            det = rd - ppost if (rd is not None and ppost is not None) else None
+            if det is not None and t > 2:
+                lat.append(det)
+            if po is not None and st and t > 2:
+                per.append(po - min(st))
+            if t < args.show:
+                print(f"  {t:3d}: {rd} {min(st) if st else None},{max(st) if st else None} "
+                      f"{min(iss) if iss else None},{max(iss) if iss else None} {max(dr) if dr else None} {po} | {det}")
+    if lat:
+        lat.sort()
+        per.sort()
+        print(json.dumps({"detect_ticks_median": lat[len(lat) // 2], "detect_ticks_p90": lat[9 * len(lat) // 10],
+                          "start_to_post_ticks_median": per[len(per) // 2]}))
+    for c in comms:
+        c.destroy()
+
+
+if __name__ == "__main__":
+    main()
