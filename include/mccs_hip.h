@@ -82,7 +82,17 @@ mccsResult_t mccs_hip_reduce_tune_grid(int blocks);
  * in KernelPlan.kernel_fn.  func: mccsFuncAllReduce | mccsFuncAllGather. */
 const void *mccs_hip_coll_kernel(int func, int dtype, int op);
 /* plan.rs:638-669 launch_plan: hipLaunchKernel(fn, grid, block, {comm,
- * channelMask, workHead}, 0, stream).  grid = #channels * lanes. */
+ * channelMask, workHead}, 0, stream).  grid = #channels * lanes; block =
+ * 96..576 threads (one wave of it is the control wave).
+ * One launch per rank, one rank per GPU (the reference deployment): ranks
+ * that share a GPU spin on each other's FIFO flags, so their kernels must be
+ * co-resident, which separate launches do not guarantee (two co-located ranks
+ * launched one after the other deadlock until the watchdog fires).  While an
+ * earlier launch of ANOTHER communicator on the current device, issued through
+ * this function by this process, is still running, the call is refused with
+ * mccsInvalidUsage and nothing is launched.  Co-located ranks go through the
+ * communicator API (mccsCommInitAll + mccsGroupStart/End), which fuses them
+ * into one launch. */
 mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, struct mccsDevComm *comm, uint64_t channelMask,
                                   struct mccsDevWork *workHead, unsigned grid, unsigned block,
                                   hipStream_t stream);

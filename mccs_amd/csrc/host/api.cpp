@@ -70,7 +70,7 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   MCCS_CHECK(validate_cfg(cfg, nranks));
   if (rank < 0 || rank >= nranks) return mccsInvalidArgument;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return mccsInvalidArgument;
+  if (rt().GetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return mccsInvalidArgument;
   Comm* c = new Comm();
   c->rank = rank;
   c->nranks = nranks;
@@ -115,14 +115,13 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
 static mccsResult_t enable_peer(int a, int b) {
   if (a == b) return mccsSuccess;
   int can = 0;
-  if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) return mccsSystemError;
+  if (rt().CanAccessPeer(&can, a, b) != hipSuccess || !can) return mccsSystemError;
   DeviceGuard g(a);
-  hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+  hipError_t e = rt().EnablePeerAccess(b);
+  if (e != hipSuccess) {
     MCCS_LOG("hipDeviceEnablePeerAccess(%d -> %d): %s", a, b, hipGetErrorString(e));
     return mccsUnhandledCudaError;
   }
-  (void)hipGetLastError();
   return mccsSuccess;
 }
 
@@ -335,12 +334,13 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
   Comm* c = (Comm*)comm;
   if (!c) return mccsInvalidArgument;
   DeviceGuard g(c->device);
-  MCCS_HIP(hipEventSynchronize(c->event));
-  if (c->stream) MCCS_HIP(hipStreamSynchronize(c->stream));
+  MCCS_HIP(rt().EventSynchronize(c->event));
+  if (c->stream) MCCS_HIP(rt().StreamSynchronize(c->stream));
   unsigned err = 0;
-  MCCS_HIP(ring_take_device_error(&err));
+  MCCS_HIP(rt().TakeDeviceError(&err, c->launched_tus));
+  c->launched_tus = 0;
   uint32_t abort_val = 0;
-  MCCS_HIP(hipMemcpy(&abort_val, c->d_abort, sizeof(abort_val), hipMemcpyDeviceToHost));
+  MCCS_HIP(rt().Memcpy(&abort_val, c->d_abort, sizeof(abort_val), hipMemcpyDeviceToHost));
   if (err || abort_val) c->failed = true;
   if (err & MCCS_ERR_TIMEOUT) return mccsTimeout;
   if (err || abort_val) return mccsRemoteError;
@@ -352,7 +352,7 @@ extern "C" mccsResult_t mccsCommAbort(mccsComm_t comm) {
   if (!c) return mccsInvalidArgument;
   DeviceGuard g(c->device);
   const uint32_t one = 1;
-  MCCS_HIP(hipMemcpy(c->d_abort, &one, sizeof(one), hipMemcpyHostToDevice));
+  MCCS_HIP(rt().Memcpy(c->d_abort, &one, sizeof(one), hipMemcpyHostToDevice));
   c->failed = true;
   return mccsSuccess;
 }

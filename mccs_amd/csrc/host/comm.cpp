@@ -104,6 +104,7 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
 // Pooling by (device, type, size) means the library never flips the type of
 // a range it owns.
 struct PooledArena {
+  unsigned generation;  // rt_generation() of the runtime that allocated it
   int device;
   bool uncached;
   size_t bytes;
@@ -115,7 +116,8 @@ static std::vector<PooledArena> g_pool;
 static char* pool_take(int device, bool uncached, size_t bytes) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
   for (size_t i = 0; i < g_pool.size(); ++i)
-    if (g_pool[i].device == device && g_pool[i].uncached == uncached && g_pool[i].bytes == bytes) {
+    if (g_pool[i].generation == rt_generation() && g_pool[i].device == device && g_pool[i].uncached == uncached &&
+        g_pool[i].bytes == bytes) {
       char* p = g_pool[i].ptr;
       g_pool.erase(g_pool.begin() + i);
       return p;
@@ -125,7 +127,7 @@ static char* pool_take(int device, bool uncached, size_t bytes) {
 
 static void pool_give(int device, bool uncached, size_t bytes, char* p) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.push_back(PooledArena{device, uncached, bytes, p});
+  g_pool.push_back(PooledArena{rt_generation(), device, uncached, bytes, p});
 }
 
 // Swap this comm's uncached arena for a plain device arena (used when IPC
@@ -136,10 +138,10 @@ mccsResult_t comm_switch_to_device_arena(Comm* c) {
   if (c->own_arena) pool_give(c->device, c->own_arena_uncached, bytes, c->own_arena);
   c->own_arena_uncached = false;
   c->own_arena = pool_take(c->device, false, bytes);
-  if (!c->own_arena) MCCS_HIP(hipMalloc((void**)&c->own_arena, bytes));
-  MCCS_HIP(hipMemset(c->own_arena, 0, bytes));
-  MCCS_HIP(ring_flush_caches(nullptr));
-  MCCS_HIP(hipDeviceSynchronize());
+  if (!c->own_arena) MCCS_HIP(rt().Malloc((void**)&c->own_arena, bytes));
+  MCCS_HIP(rt().Memset(c->own_arena, 0, bytes));
+  MCCS_HIP(rt().FlushCaches());
+  MCCS_HIP(rt().DeviceSynchronize());
   c->peer_arena[c->rank] = c->own_arena;
   return mccsSuccess;
 }
@@ -156,7 +158,7 @@ mccsResult_t comm_alloc_local(Comm* c) {
     if (c->own_arena) {
       c->own_arena_uncached = true;
     } else {
-      hipError_t e = hipExtMallocWithFlags((void**)&c->own_arena, bytes, hipDeviceMallocUncached);
+      hipError_t e = rt().MallocUncached((void**)&c->own_arena, bytes);
       if (e == hipSuccess) {
         c->own_arena_uncached = true;
       } else {
@@ -168,58 +170,50 @@ mccsResult_t comm_alloc_local(Comm* c) {
   }
   if (!c->own_arena) {
     c->own_arena = pool_take(c->device, false, bytes);
-    if (!c->own_arena) MCCS_HIP(hipMalloc((void**)&c->own_arena, bytes));
+    if (!c->own_arena) MCCS_HIP(rt().Malloc((void**)&c->own_arena, bytes));
   }
-  if (c->own_arena_uncached) {
-    // trust but verify: the runtime must report the uncached allocation flag
-    hipPointerAttribute_t attr;
-    std::memset(&attr, 0, sizeof(attr));
-    if (hipPointerGetAttributes(&attr, c->own_arena) != hipSuccess ||
-        attr.allocationFlags != hipDeviceMallocUncached) {
-      (void)hipGetLastError();
-      MCCS_LOG("arena %p reports allocationFlags=0x%x, not uncached: using system fences", (void*)c->own_arena,
-               attr.allocationFlags);
-      c->own_arena_uncached = false;
-    }
+  // trust but verify: the runtime must report the uncached allocation flag
+  if (c->own_arena_uncached && !rt().IsUncached(c->own_arena)) {
+    MCCS_LOG("arena %p is not reported uncached: using system fences", (void*)c->own_arena);
+    c->own_arena_uncached = false;
   }
   if (std::getenv("MCCS_DEBUG"))
     MCCS_LOG("rank %d arena %p bytes %zu uncached=%d", c->rank, (void*)c->own_arena, bytes,
              (int)c->own_arena_uncached);
-  MCCS_HIP(hipMemset(c->own_arena, 0, bytes));
-  MCCS_HIP(ring_flush_caches(nullptr));
-  MCCS_HIP(hipDeviceSynchronize());
+  MCCS_HIP(rt().Memset(c->own_arena, 0, bytes));
+  MCCS_HIP(rt().FlushCaches());
+  MCCS_HIP(rt().DeviceSynchronize());
   c->peer_arena.assign(c->nranks, nullptr);
   c->peer_opened_ipc.assign(c->nranks, false);
   c->peer_arena[c->rank] = c->own_arena;
 
-  MCCS_HIP(hipMalloc((void**)&c->d_abort, 64));
-  MCCS_HIP(hipMemset(c->d_abort, 0, 64));  // the reference leaves it uninitialised (device.rs:157)
-  MCCS_HIP(hipMalloc((void**)&c->d_comm, sizeof(mccsDevCommAndChannels)));
+  MCCS_HIP(rt().Malloc((void**)&c->d_abort, 64));
+  MCCS_HIP(rt().Memset(c->d_abort, 0, 64));  // the reference leaves it uninitialised (device.rs:157)
+  MCCS_HIP(rt().Malloc((void**)&c->d_comm, sizeof(mccsDevCommAndChannels)));
   c->d_peers.assign(c->nch, nullptr);
   c->d_user_ranks.assign(c->nch, nullptr);
   for (int ch = 0; ch < c->nch; ++ch) {
-    MCCS_HIP(hipMalloc((void**)&c->d_peers[ch], sizeof(mccsDevChannelPeer) * c->nranks));
-    MCCS_HIP(hipMalloc((void**)&c->d_user_ranks[ch], sizeof(int) * c->nranks));
+    MCCS_HIP(rt().Malloc((void**)&c->d_peers[ch], sizeof(mccsDevChannelPeer) * c->nranks));
+    MCCS_HIP(rt().Malloc((void**)&c->d_user_ranks[ch], sizeof(int) * c->nranks));
   }
   c->work_depth = (uint32_t)c->cfg.work_fifo_depth;
-  MCCS_HIP(hipHostMalloc((void**)&c->h_work, sizeof(mccsDevWork) * c->work_depth, hipHostMallocMapped));
-  MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_work, c->h_work, 0));
+  MCCS_HIP(rt().HostMallocMapped((void**)&c->h_work, sizeof(mccsDevWork) * c->work_depth));
+  MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_work, c->h_work));
   std::memset(c->h_work, 0, sizeof(mccsDevWork) * c->work_depth);
-  MCCS_HIP(hipHostMalloc((void**)&c->h_graph_work, sizeof(mccsDevWork) * Comm::kGraphWorkEntries,
-                         hipHostMallocMapped));
-  MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_graph_work, c->h_graph_work, 0));
+  MCCS_HIP(rt().HostMallocMapped((void**)&c->h_graph_work, sizeof(mccsDevWork) * Comm::kGraphWorkEntries));
+  MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_graph_work, c->h_graph_work));
   std::memset(c->h_graph_work, 0, sizeof(mccsDevWork) * Comm::kGraphWorkEntries);
   c->graph_work_used = 0;
-  MCCS_HIP(hipHostMalloc((void**)&c->h_done, sizeof(uint32_t) * MCCS_MAX_NCHANNELS, hipHostMallocMapped));
-  MCCS_HIP(hipHostGetDevicePointer((void**)&c->d_done, c->h_done, 0));
+  MCCS_HIP(rt().HostMallocMapped((void**)&c->h_done, sizeof(uint32_t) * MCCS_MAX_NCHANNELS));
+  MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_done, c->h_done));
   std::memset(c->h_done, 0, sizeof(uint32_t) * MCCS_MAX_NCHANNELS);
   c->chan_next.assign(c->nch, 0);
   c->work_next = 0;
   c->work_acked_min = 0;
   // comm stream: created on first use (comm_stream); the event becomes
   // interprocess only when a backend exports it (comm_make_event_ipc)
-  MCCS_HIP(hipEventCreateWithFlags(&c->event, hipEventDisableTiming));
-  MCCS_HIP(hipEventCreateWithFlags(&c->user_event, hipEventDisableTiming));
+  MCCS_HIP(rt().EventCreate(&c->event, hipEventDisableTiming));
+  MCCS_HIP(rt().EventCreate(&c->user_event, hipEventDisableTiming));
   c->sched.assign(c->nch, ChannelSchedule{});
   return mccsSuccess;
 }
@@ -262,8 +256,8 @@ mccsResult_t comm_build_device(Comm* c) {
       r.tail = (uint64_t*)(me + L.tail_off(ch));
       r.head = (uint64_t*)(pv + L.head_off(ch));
     }
-    MCCS_HIP(hipMemcpy(c->d_peers[ch], peers.data(), sizeof(mccsDevChannelPeer) * n, hipMemcpyHostToDevice));
-    MCCS_HIP(hipMemcpy(c->d_user_ranks[ch], user_ranks.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    MCCS_HIP(rt().Memcpy(c->d_peers[ch], peers.data(), sizeof(mccsDevChannelPeer) * n, hipMemcpyHostToDevice));
+    MCCS_HIP(rt().Memcpy(c->d_user_ranks[ch], user_ranks.data(), sizeof(int) * n, hipMemcpyHostToDevice));
     mccsDevChannel& dc = hc.channels[ch];
     dc.peers = c->d_peers[ch];
     dc.ring.prev = prev;
@@ -272,7 +266,7 @@ mccsResult_t comm_build_device(Comm* c) {
     dc.ring.index = (ix_rank + n - ix_zero) % n;
     dc.workFifoDone = c->d_done + ch;
   }
-  MCCS_HIP(hipMemcpy(c->d_comm, &hc, sizeof(hc), hipMemcpyHostToDevice));
+  MCCS_HIP(rt().Memcpy(c->d_comm, &hc, sizeof(hc), hipMemcpyHostToDevice));
   MCCS_CHECK(comm_set_kernel_cfg(c));
   c->connected = true;
   return mccsSuccess;
@@ -281,7 +275,7 @@ mccsResult_t comm_build_device(Comm* c) {
 mccsResult_t comm_stream(Comm* c, hipStream_t* out) {
   if (!c->stream) {
     DeviceGuard g(c->device);
-    MCCS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    MCCS_HIP(rt().StreamCreate(&c->stream));
   }
   *out = c->stream;
   return mccsSuccess;
@@ -306,21 +300,21 @@ mccsResult_t comm_make_event_ipc(Comm* c) {
 mccsResult_t comm_free(Comm* c) {
   DeviceGuard g(c->device);
   // the last launch (any stream) must be done before its arenas are reused
-  if (c->event) (void)hipEventSynchronize(c->event);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->event) (void)rt().EventSynchronize(c->event);
+  if (c->stream) (void)rt().StreamSynchronize(c->stream);
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
     if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)hipIpcCloseMemHandle(c->peer_arena[r]);
   if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->layout.total(), c->own_arena);
-  for (auto p : c->d_peers) (void)hipFree(p);
-  for (auto p : c->d_user_ranks) (void)hipFree(p);
-  if (c->d_comm) (void)hipFree(c->d_comm);
-  if (c->d_abort) (void)hipFree(c->d_abort);
-  if (c->h_work) (void)hipHostFree(c->h_work);
-  if (c->h_graph_work) (void)hipHostFree(c->h_graph_work);
-  if (c->h_done) (void)hipHostFree(c->h_done);
-  if (c->event) (void)hipEventDestroy(c->event);
-  if (c->user_event) (void)hipEventDestroy(c->user_event);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (auto p : c->d_peers) (void)rt().Free(p);
+  for (auto p : c->d_user_ranks) (void)rt().Free(p);
+  if (c->d_comm) (void)rt().Free(c->d_comm);
+  if (c->d_abort) (void)rt().Free(c->d_abort);
+  if (c->h_work) (void)rt().HostFree(c->h_work);
+  if (c->h_graph_work) (void)rt().HostFree(c->h_graph_work);
+  if (c->h_done) (void)rt().HostFree(c->h_done);
+  if (c->event) (void)rt().EventDestroy(c->event);
+  if (c->user_event) (void)rt().EventDestroy(c->user_event);
+  if (c->stream) (void)rt().StreamDestroy(c->stream);
   return mccsSuccess;
 }
 

@@ -132,7 +132,7 @@ static mccsResult_t wait_work_queue(Comm* c, uint32_t target) {
       if (ackd[ch] == c->chan_next[ch]) __atomic_store_n(&c->h_done[ch], all, __ATOMIC_RELAXED);
     c->work_acked_min = all;
     if (!rolling_less_u32(c->work_acked_min + c->work_depth, target)) return mccsSuccess;
-    if ((spins & 0xfffff) == 0xfffff && hipEventQuery(c->event) == hipSuccess) {
+    if ((spins & 0xfffff) == 0xfffff && rt().EventQuery(c->event) == hipSuccess) {
       // stream idle but acks missing: the kernel aborted
       return mccsRemoteError;
     }
@@ -259,11 +259,11 @@ int coresident_ring_blocks(int block, int device) {
   }
   DeviceGuard g(device);
   int ncu = 0;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  if (rt().CuCount(&ncu, device) != hipSuccess) return 0;
   int best = 1 << 30;
   auto probe = [&](const void* fn) {
     int per_cu = 0;
-    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, 0) != hipSuccess) per_cu = 0;
+    if (!fn || rt().BlocksPerCu(&per_cu, fn, block) != hipSuccess) per_cu = 0;
     best = std::min(best, per_cu);
   };
   probe(ring_multi_kernel_ptr(mccsFuncAllGather, mccsInt8, 0));
@@ -299,9 +299,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     }
     // A capturing stream records this launch into a HIP graph: its work
     // list must outlive the FIFO's rolling slots (upload_work_graph).
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    MCCS_HIP(hipStreamIsCapturing(user_streams[idx[0]], &cap));
-    const bool capturing = cap == hipStreamCaptureStatusActive;
+    bool capturing = false;
+    MCCS_HIP(rt().StreamIsCapturing(user_streams[idx[0]], &capturing));
     std::vector<LaunchDesc> lds(idx.size());
     for (size_t k = 0; k < idx.size(); ++k)
       MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k]) : upload_work(comms[idx[k]], &lds[k]));
@@ -315,8 +314,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     if (events) {
       for (size_t k = 0; k < idx.size(); ++k) {
         Comm* c = comms[idx[k]];
-        MCCS_HIP(hipEventRecord(c->user_event, user_streams[idx[k]]));
-        MCCS_HIP(hipStreamWaitEvent(st, c->user_event, 0));
+        MCCS_HIP(rt().EventRecord(c->user_event, user_streams[idx[k]]));
+        MCCS_HIP(rt().StreamWaitEvent(st, c->user_event));
       }
     }
     const unsigned grid = (unsigned)(lds[0].nch_used * c0->lanes);
@@ -335,6 +334,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
           ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps)
         return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
       ma.comm[k] = (mccsDevComm*)ck->d_comm;
+      comms[idx[k]]->launched_tus |= 1u << ring_tu_index(ck->plan_func, ck->plan_op);
       ma.work[k] = lds[k].work;
       if (ck->kcfg.fence_mode != MCCS_FENCE_UNCACHED) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
       ma.cfg.timeout_ticks = (ma.cfg.timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)
@@ -343,15 +343,15 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       ma.cfg.profile |= ck->kcfg.profile;
     }
     void* args[1] = {&ma};
-    MCCS_HIP(hipLaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, 0, st));
-    MCCS_HIP(hipEventRecord(c0->event, st));
+    MCCS_HIP(rt().LaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, st));
+    MCCS_HIP(rt().EventRecord(c0->event, st));
     if (events) {
       for (size_t k = 0; k < idx.size(); ++k) {
         if (!bridge && k == 0) continue;
-        MCCS_HIP(hipStreamWaitEvent(user_streams[idx[k]], c0->event, 0));
+        MCCS_HIP(rt().StreamWaitEvent(user_streams[idx[k]], c0->event));
       }
     }
-    for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(hipEventRecord(comms[idx[k]]->event, st));
+    for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
   }
   return mccsSuccess;
 }

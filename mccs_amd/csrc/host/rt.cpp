@@ -1,0 +1,303 @@
+// rt.cpp — HIP implementation of the device-runtime seam (rt.h) and the
+// recording fake CPU tests install to drive the multi-device path without
+// GPUs.
+#include "rt.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+
+#include "comm.h"
+
+namespace mccs {
+
+namespace {
+
+class HipRuntime final : public DeviceRuntime {
+ public:
+  hipError_t GetDeviceCount(int* n) override { return hipGetDeviceCount(n); }
+  hipError_t GetDevice(int* d) override { return hipGetDevice(d); }
+  hipError_t SetDevice(int d) override { return hipSetDevice(d); }
+  hipError_t Malloc(void** p, size_t bytes) override { return hipMalloc(p, bytes); }
+  hipError_t MallocUncached(void** p, size_t bytes) override {
+    return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+  }
+  bool IsUncached(void* p) override {
+    hipPointerAttribute_t attr;
+    std::memset(&attr, 0, sizeof(attr));
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return attr.allocationFlags == hipDeviceMallocUncached;
+  }
+  hipError_t Free(void* p) override { return hipFree(p); }
+  hipError_t Memset(void* p, int v, size_t bytes) override { return hipMemset(p, v, bytes); }
+  hipError_t Memcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) override {
+    return hipMemcpy(dst, src, bytes, kind);
+  }
+  hipError_t HostMallocMapped(void** p, size_t bytes) override { return hipHostMalloc(p, bytes, hipHostMallocMapped); }
+  hipError_t HostGetDevicePointer(void** d, void* h) override { return hipHostGetDevicePointer(d, h, 0); }
+  hipError_t HostFree(void* p) override { return hipHostFree(p); }
+  hipError_t DeviceSynchronize() override { return hipDeviceSynchronize(); }
+  hipError_t FlushCaches() override { return ring_flush_caches(nullptr); }
+  hipError_t CanAccessPeer(int* can, int dev, int peer) override { return hipDeviceCanAccessPeer(can, dev, peer); }
+  hipError_t EnablePeerAccess(int peer) override {
+    hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) e = hipSuccess;
+    (void)hipGetLastError();
+    return e;
+  }
+  hipError_t EventCreate(hipEvent_t* e, unsigned flags) override { return hipEventCreateWithFlags(e, flags); }
+  hipError_t EventDestroy(hipEvent_t e) override { return hipEventDestroy(e); }
+  hipError_t EventRecord(hipEvent_t e, hipStream_t s) override { return hipEventRecord(e, s); }
+  hipError_t EventSynchronize(hipEvent_t e) override { return hipEventSynchronize(e); }
+  hipError_t EventQuery(hipEvent_t e) override { return hipEventQuery(e); }
+  hipError_t StreamCreate(hipStream_t* s) override { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
+  hipError_t StreamDestroy(hipStream_t s) override { return hipStreamDestroy(s); }
+  hipError_t StreamSynchronize(hipStream_t s) override { return hipStreamSynchronize(s); }
+  hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) override { return hipStreamWaitEvent(s, e, 0); }
+  hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) override {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    hipError_t e = hipStreamIsCapturing(s, &st);
+    *capturing = st == hipStreamCaptureStatusActive;
+    return e;
+  }
+  hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
+    return hipLaunchKernel(fn, grid, block, args, 0, s);
+  }
+  hipError_t BlocksPerCu(int* per_cu, const void* fn, int block) override {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, block, 0);
+  }
+  hipError_t CuCount(int* ncu, int device) override {
+    return hipDeviceGetAttribute(ncu, hipDeviceAttributeMultiprocessorCount, device);
+  }
+  hipError_t TakeDeviceError(unsigned* err, unsigned tu_mask) override { return ring_take_device_error(err, tu_mask); }
+};
+
+// Recording fake: "device" memory is host memory tagged with its device,
+// nothing executes, and every call that orders work or makes the host wait
+// is appended to a text log (one event per line):
+//   launch dev=D grid=XxY block=B stream=S comms_on_dev=1
+//   record dev=D event=E stream=S          stream_wait dev=D stream=S event=E event_dev=D2
+//   host_wait what=event|stream|device|memcpy|error dev=D
+//   peer dev=D peer=P                      flush dev=D
+class FakeRuntime final : public DeviceRuntime {
+ public:
+  explicit FakeRuntime(int ndev) : ndev_(ndev) {}
+  ~FakeRuntime() override {
+    for (auto& kv : mem_) std::free(kv.first);
+  }
+  std::string log() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return log_.str();
+  }
+  void clear() {
+    std::lock_guard<std::mutex> lk(mu_);
+    log_.str("");
+  }
+  hipError_t GetDeviceCount(int* n) override {
+    *n = ndev_;
+    return hipSuccess;
+  }
+  hipError_t GetDevice(int* d) override {
+    *d = cur_;
+    return hipSuccess;
+  }
+  hipError_t SetDevice(int d) override {
+    if (d < 0 || d >= ndev_) return hipErrorInvalidDevice;
+    cur_ = d;
+    return hipSuccess;
+  }
+  hipError_t Malloc(void** p, size_t bytes) override { return alloc(p, bytes, false); }
+  hipError_t MallocUncached(void** p, size_t bytes) override { return alloc(p, bytes, true); }
+  bool IsUncached(void* p) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = mem_.find(p);
+    return it != mem_.end() && it->second.uncached;
+  }
+  hipError_t Free(void* p) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = mem_.find(p);
+    if (it == mem_.end()) return hipErrorInvalidValue;
+    std::free(p);
+    mem_.erase(it);
+    return hipSuccess;
+  }
+  hipError_t Memset(void* p, int v, size_t bytes) override {
+    std::memset(p, v, bytes);
+    return hipSuccess;
+  }
+  hipError_t Memcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind) override {
+    std::memcpy(dst, src, bytes);
+    note("host_wait what=memcpy dev=" + std::to_string(cur_));
+    return hipSuccess;
+  }
+  hipError_t HostMallocMapped(void** p, size_t bytes) override { return alloc(p, bytes, false); }
+  hipError_t HostGetDevicePointer(void** d, void* h) override {
+    *d = h;
+    return hipSuccess;
+  }
+  hipError_t HostFree(void* p) override { return Free(p); }
+  hipError_t DeviceSynchronize() override {
+    note("host_wait what=device dev=" + std::to_string(cur_));
+    return hipSuccess;
+  }
+  hipError_t FlushCaches() override {
+    note("flush dev=" + std::to_string(cur_));
+    return hipSuccess;
+  }
+  hipError_t CanAccessPeer(int* can, int dev, int peer) override {
+    *can = dev >= 0 && dev < ndev_ && peer >= 0 && peer < ndev_;
+    return hipSuccess;
+  }
+  hipError_t EnablePeerAccess(int peer) override {
+    note("peer dev=" + std::to_string(cur_) + " peer=" + std::to_string(peer));
+    return hipSuccess;
+  }
+  hipError_t EventCreate(hipEvent_t* e, unsigned) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    const uintptr_t id = ++next_id_;
+    events_[id] = cur_;
+    *e = (hipEvent_t)id;
+    return hipSuccess;
+  }
+  hipError_t EventDestroy(hipEvent_t e) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    events_.erase((uintptr_t)e);
+    return hipSuccess;
+  }
+  hipError_t EventRecord(hipEvent_t e, hipStream_t s) override {
+    note("record dev=" + std::to_string(cur_) + " event=" + std::to_string((uintptr_t)e) + " stream=" + sid(s));
+    return hipSuccess;
+  }
+  hipError_t EventSynchronize(hipEvent_t e) override {
+    note("host_wait what=event dev=" + std::to_string(event_dev(e)) + " event=" + std::to_string((uintptr_t)e));
+    return hipSuccess;
+  }
+  hipError_t EventQuery(hipEvent_t) override { return hipSuccess; }
+  hipError_t StreamCreate(hipStream_t* s) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    *s = (hipStream_t)(++next_id_);
+    return hipSuccess;
+  }
+  hipError_t StreamDestroy(hipStream_t) override { return hipSuccess; }
+  hipError_t StreamSynchronize(hipStream_t s) override {
+    note("host_wait what=stream dev=" + std::to_string(cur_) + " stream=" + sid(s));
+    return hipSuccess;
+  }
+  hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) override {
+    note("stream_wait dev=" + std::to_string(cur_) + " stream=" + sid(s) + " event=" +
+         std::to_string((uintptr_t)e) + " event_dev=" + std::to_string(event_dev(e)));
+    return hipSuccess;
+  }
+  hipError_t StreamIsCapturing(hipStream_t, bool* capturing) override {
+    *capturing = false;
+    return hipSuccess;
+  }
+  hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
+    // every communicator of a fused ring launch must live on the launching device
+    bool on_dev = true;
+    if (fn && args && grid.y >= 1 && grid.y <= MCCS_MULTI_MAX_RANKS) {
+      const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
+      for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(ma->comm[k]) == cur_;
+    }
+    note("launch dev=" + std::to_string(cur_) + " grid=" + std::to_string(grid.x) + "x" + std::to_string(grid.y) +
+         " block=" + std::to_string(block.x) + " stream=" + sid(s) + " comms_on_dev=" + (on_dev ? "1" : "0"));
+    return hipSuccess;
+  }
+  hipError_t BlocksPerCu(int* per_cu, const void*, int) override {
+    *per_cu = 1;
+    return hipSuccess;
+  }
+  hipError_t CuCount(int* ncu, int) override {
+    *ncu = 256;
+    return hipSuccess;
+  }
+  hipError_t TakeDeviceError(unsigned* err, unsigned) override {
+    *err = 0;
+    note("host_wait what=error dev=" + std::to_string(cur_));
+    return hipSuccess;
+  }
+
+ private:
+  struct Block {
+    int device;
+    bool uncached;
+  };
+  hipError_t alloc(void** p, size_t bytes, bool uncached) {
+    void* q = std::calloc(1, bytes ? bytes : 1);
+    if (!q) return hipErrorOutOfMemory;
+    std::lock_guard<std::mutex> lk(mu_);
+    mem_[q] = Block{cur_, uncached};
+    *p = q;
+    return hipSuccess;
+  }
+  int dev_of(const void* p) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = mem_.find(const_cast<void*>(p));
+    return it == mem_.end() ? -1 : it->second.device;
+  }
+  int event_dev(hipEvent_t e) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = events_.find((uintptr_t)e);
+    return it == events_.end() ? -1 : it->second;
+  }
+  static std::string sid(hipStream_t s) { return std::to_string((uintptr_t)s); }
+  void note(const std::string& line) {
+    std::lock_guard<std::mutex> lk(mu_);
+    log_ << line << '\n';
+  }
+  int ndev_, cur_ = 0;
+  uintptr_t next_id_ = 0;
+  std::mutex mu_;
+  std::map<void*, Block> mem_;
+  std::map<uintptr_t, int> events_;
+  std::ostringstream log_;
+};
+
+HipRuntime g_hip;
+std::unique_ptr<FakeRuntime> g_fake;
+unsigned g_generation = 0;
+
+}  // namespace
+
+DeviceRuntime& rt() { return g_fake ? (DeviceRuntime&)*g_fake : (DeviceRuntime&)g_hip; }
+
+void rt_use_fake(int ndevices) {
+  ++g_generation;
+  if (ndevices > 0) g_fake.reset(new FakeRuntime(ndevices));
+  else g_fake.reset();
+}
+
+unsigned rt_generation() { return g_generation; }
+
+}  // namespace mccs
+
+// ---- test-only C-ABI (tests/test_multidevice_launch.py) -------------------
+// Installs (ndevices > 0) or removes (0) the recording fake runtime.  Only
+// communicators created while it is installed may be used with it.
+extern "C" mccsResult_t mccs_test_fake_runtime(int ndevices) {
+  if (ndevices < 0 || ndevices > 64) return mccsInvalidArgument;
+  mccs::rt_use_fake(ndevices);
+  return mccsSuccess;
+}
+
+// Copies the fake runtime's event log (NUL-terminated, truncated to cap) and
+// optionally clears it; returns the log length, or -1 without a fake.
+extern "C" int mccs_test_fake_log(char* buf, int cap, int clear) {
+  if (!mccs::g_fake) return -1;
+  const std::string s = mccs::g_fake->log();
+  if (buf && cap > 0) {
+    const size_t n = std::min(s.size(), (size_t)cap - 1);
+    std::memcpy(buf, s.data(), n);
+    buf[n] = '\0';
+  }
+  if (clear) mccs::g_fake->clear();
+  return (int)s.size();
+}

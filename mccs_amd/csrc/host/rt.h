@@ -1,0 +1,59 @@
+// rt.h — the device-runtime seam of the host path (internal).
+//
+// Every HIP call the communicator lifecycle makes on the single-process path
+// (mccsCommInitAll -> group launch -> mccsCommSync -> destroy) goes through
+// rt(): the HIP runtime in production, or a recording fake with N pretend
+// devices (host memory, no kernels run) that CPU tests install with
+// mccs_test_fake_runtime() to check how launches are issued across devices
+// (tests/test_multidevice_launch.py).  The IPC (one rank per process) and
+// shared-memory service paths call HIP directly: they need a real GPU.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace mccs {
+
+class DeviceRuntime {
+ public:
+  virtual ~DeviceRuntime() = default;
+  virtual hipError_t GetDeviceCount(int* n) = 0;
+  virtual hipError_t GetDevice(int* d) = 0;
+  virtual hipError_t SetDevice(int d) = 0;
+  virtual hipError_t Malloc(void** p, size_t bytes) = 0;
+  virtual hipError_t MallocUncached(void** p, size_t bytes) = 0;
+  virtual bool IsUncached(void* p) = 0;  // the runtime reports hipDeviceMallocUncached
+  virtual hipError_t Free(void* p) = 0;
+  virtual hipError_t Memset(void* p, int v, size_t bytes) = 0;
+  virtual hipError_t Memcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) = 0;
+  virtual hipError_t HostMallocMapped(void** p, size_t bytes) = 0;
+  virtual hipError_t HostGetDevicePointer(void** d, void* h) = 0;
+  virtual hipError_t HostFree(void* p) = 0;
+  virtual hipError_t DeviceSynchronize() = 0;
+  virtual hipError_t FlushCaches() = 0;  // ring_flush_caches on the null stream of the current device
+  virtual hipError_t CanAccessPeer(int* can, int dev, int peer) = 0;
+  virtual hipError_t EnablePeerAccess(int peer) = 0;  // from the current device; already-enabled is success
+  virtual hipError_t EventCreate(hipEvent_t* e, unsigned flags) = 0;
+  virtual hipError_t EventDestroy(hipEvent_t e) = 0;
+  virtual hipError_t EventRecord(hipEvent_t e, hipStream_t s) = 0;
+  virtual hipError_t EventSynchronize(hipEvent_t e) = 0;
+  virtual hipError_t EventQuery(hipEvent_t e) = 0;
+  virtual hipError_t StreamCreate(hipStream_t* s) = 0;  // non-blocking
+  virtual hipError_t StreamDestroy(hipStream_t s) = 0;
+  virtual hipError_t StreamSynchronize(hipStream_t s) = 0;
+  virtual hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) = 0;
+  virtual hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) = 0;
+  virtual hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) = 0;
+  virtual hipError_t BlocksPerCu(int* per_cu, const void* fn, int block) = 0;
+  virtual hipError_t CuCount(int* ncu, int device) = 0;
+  virtual hipError_t TakeDeviceError(unsigned* err, unsigned tu_mask) = 0;
+};
+
+DeviceRuntime& rt();
+// Installs a recording fake with `ndevices` devices (0 restores HIP).
+void rt_use_fake(int ndevices);
+// Bumped by every rt_use_fake: memory pooled under one runtime is never
+// handed out under another.
+unsigned rt_generation();
+
+}  // namespace mccs

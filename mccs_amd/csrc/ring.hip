@@ -4,6 +4,9 @@
 // reduction op, compiled in parallel).
 #include "ring_kernel.h"
 
+#include <mutex>
+#include <vector>
+
 extern "C" __global__ void __launch_bounds__(MCCS_RING_MAX_THREADS)
     mccsKernel_AllGather_RING_SIMPLE_Sum_int8_t(mccsDevComm* comm, uint64_t channelMask, mccsDevWork* workHead) {
   mccs::ring_kernel_body<mccsFuncAllGather, mccsInt8, mccs::OpSum>(comm, channelMask, workHead, blockIdx.x,
@@ -81,14 +84,19 @@ hipError_t ring_read_profile(unsigned long long* out, bool reset) {
   return hipSuccess;
 }
 
-// ORs (and clears) the device error words of every ring translation unit.
-hipError_t ring_take_device_error(unsigned* err) {
+// Translation unit of a collective's kernels: 0 AllGather, 1 + op AllReduce.
+int ring_tu_index(int func, int op) { return func == mccsFuncAllGather ? 0 : 1 + (op & 3); }
+
+// ORs (and clears) the device error words of the ring translation units in
+// tu_mask: one device read per kind of kernel a communicator launched.
+hipError_t ring_take_device_error(unsigned* err, unsigned tu_mask) {
   *err = 0;
   hipError_t (*const takers[])(unsigned*) = {ring_tu_ag_take_error, ring_tu_ar_sum_take_error,
                                              ring_tu_ar_prod_take_error, ring_tu_ar_max_take_error,
                                              ring_tu_ar_min_take_error};
-  for (auto tk : takers) {
-    hipError_t e = tk(err);
+  for (int i = 0; i < 5; ++i) {
+    if (!(tu_mask >> i & 1)) continue;
+    hipError_t e = takers[i](err);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -100,6 +108,42 @@ extern "C" const void* mccs_hip_coll_kernel(int func, int dtype, int op) {
   return mccs::ring_kernel_ptr(func, dtype, op);
 }
 
+namespace {
+// External launches still in flight, per device: a rank of another
+// communicator on the same device must not be launched beside them
+// (mccs_hip.h: co-located ranks need one fused launch).
+struct ExtLaunch {
+  int device;
+  const mccsDevComm* comm;
+  hipEvent_t done;
+};
+std::mutex g_ext_mu;
+std::vector<ExtLaunch> g_ext;
+
+// true if another communicator's external launch on `device` is unfinished;
+// forgets finished ones
+bool colocated_launch_running(int device, const mccsDevComm* comm) {
+  bool busy = false;
+  for (size_t i = 0; i < g_ext.size();) {
+    ExtLaunch& x = g_ext[i];
+    if (x.device == device && x.comm != comm) {
+      const hipError_t q = hipEventQuery(x.done);
+      if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        busy = true;
+        ++i;
+        continue;
+      }
+      (void)hipEventDestroy(x.done);
+      g_ext.erase(g_ext.begin() + i);
+      continue;
+    }
+    ++i;
+  }
+  return busy;
+}
+}  // namespace
+
 extern "C" mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, mccsDevComm* comm, uint64_t channelMask,
                                              mccsDevWork* workHead, unsigned grid, unsigned block,
                                              hipStream_t stream) {
@@ -107,7 +151,24 @@ extern "C" mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, mccsDe
   // blocks of one wave have no control wave (ring_kernel.h); the reference
   // host never launches fewer than 96 threads (get_task_schema, plan.rs:602-635)
   if (!fn || !comm || !workHead || grid == 0 || block <= 64 || block > MCCS_RING_MAX_THREADS) return mccsInvalidArgument;
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return mccsUnhandledCudaError;
+  std::lock_guard<std::mutex> lk(g_ext_mu);
+  if (colocated_launch_running(device, comm)) return mccsInvalidUsage;
   void* args[3] = {&comm, &channelMask, &workHead};
   hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, stream);
-  return e == hipSuccess ? mccsSuccess : mccsUnhandledCudaError;
+  if (e != hipSuccess) return mccsUnhandledCudaError;
+  // remember this launch until it completes (replacing this comm's previous one)
+  for (size_t i = 0; i < g_ext.size(); ++i)
+    if (g_ext[i].device == device && g_ext[i].comm == comm) {
+      (void)hipEventDestroy(g_ext[i].done);
+      g_ext.erase(g_ext.begin() + i);
+      break;
+    }
+  hipEvent_t done = nullptr;
+  if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(done, stream) != hipSuccess)
+    return mccsUnhandledCudaError;
+  g_ext.push_back(ExtLaunch{device, comm, done});
+  return mccsSuccess;
 }

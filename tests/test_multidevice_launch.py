@@ -1,0 +1,154 @@
+"""The one-process multi-GPU path on CPU.
+
+The reference deploys one service process that drives every GPU of the node
+(src/mccs/src/transport/shm/transporter.rs:76-78; launches per device in
+src/mccs/src/proxy/plan.rs:638-669).  Here that path is mccsCommInitAll over
+distinct devices + a grouped collective + mccsCommSync.  Its hazard is the
+deadlock class DESIGN.md records for ranks launched separately: ring blocks of
+different ranks spin on each other's flags, so every rank's kernel must be in
+flight before the host waits on any of them, and ranks sharing a GPU must be
+one launch.  These tests install the recording fake device runtime
+(csrc/host/rt.cpp, mccs_test_fake_runtime: host memory, no kernels run) with
+8 devices and check the order of launches, stream waits and host waits the
+library issues.
+"""
+import ctypes
+
+import pytest
+
+from mccs_amd import _lib
+from mccs_amd import comm as C
+
+F32, SUM = 7, 0
+
+
+def _parse(line):
+    kind, *kv = line.split()
+    return kind, dict(x.split("=", 1) for x in kv)
+
+
+@pytest.fixture
+def fake():
+    lib = _lib.load()
+
+    def install(ndev):
+        assert lib.mccs_test_fake_runtime(ndev) == 0
+
+    yield install
+    lib.mccs_test_fake_runtime(0)
+
+
+def _log(clear=True):
+    lib = _lib.load()
+    n = lib.mccs_test_fake_log(None, 0, 0)
+    assert n >= 0, "fake runtime not installed"
+    buf = ctypes.create_string_buffer(n + 1)
+    lib.mccs_test_fake_log(buf, n + 1, 1 if clear else 0)
+    return [_parse(x) for x in buf.value.decode().splitlines() if x]
+
+
+def _allreduce_group(comms, count=1 << 20):
+    with C.group():
+        for r, c in enumerate(comms):
+            # "device" buffers are never touched by the fake; distinct fake addresses
+            C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, count, F32, SUM, stream=0)
+
+
+def _check_launch_phase(ev, ndev, ranks_per_dev, lanes_x_ch):
+    launches = [(i, kv) for i, (k, kv) in enumerate(ev) if k == "launch"]
+    assert sorted(int(kv["dev"]) for _, kv in launches) == list(range(ndev)), ev
+    for _, kv in launches:
+        gx, gy = (int(v) for v in kv["grid"].split("x"))
+        assert gy == ranks_per_dev and gx == lanes_x_ch
+        assert kv["comms_on_dev"] == "1", "a fused launch carries a communicator of another device"
+    last = max(i for i, _ in launches)
+    waits = [i for i, (k, _) in enumerate(ev) if k == "host_wait"]
+    assert not waits or min(waits) > last, f"host waited before every rank was launched: {ev}"
+    for k, kv in ev:
+        if k == "stream_wait":
+            assert kv["event_dev"] == kv["dev"], f"cross-device stream dependency between launches: {kv}"
+    return launches
+
+
+def test_init_all_eight_devices_one_launch_per_device(fake):
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
+    try:
+        ev = _log()
+        # every device can reach every other device's FIFO arena
+        peers = {(int(kv["dev"]), int(kv["peer"])) for k, kv in ev if k == "peer"}
+        assert peers == {(a, b) for a in range(8) for b in range(8) if a != b}
+        lanes, nch = comms[0].lanes, comms[0].nchannels
+        assert nch == 6 and lanes == 10  # 3 edge-disjoint Hamiltonian cycles of K8, both directions
+        _allreduce_group(comms)
+        ev = _log()
+        launches = _check_launch_phase(ev, 8, 1, nch * lanes)
+        assert len(launches) == 8
+        for c in comms:
+            c.sync()
+        ev = _log()
+        assert [k for k, _ in ev if k == "launch"] == []
+        assert {int(kv["dev"]) for k, kv in ev if k == "host_wait"} == set(range(8))
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_back_to_back_groups_issue_without_host_waits(fake):
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
+    try:
+        _log()
+        for _ in range(3):
+            _allreduce_group(comms)
+        ev = _log()
+        assert sum(1 for k, _ in ev if k == "launch") == 24
+        assert not any(k == "host_wait" for k, _ in ev), "stream-ordered collectives made the host wait"
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_colocated_ranks_are_fused_per_device(fake):
+    """Two ranks per device (4 devices): one launch per device, blockIdx.y = rank slot."""
+    fake(4)
+    devs = [0, 0, 1, 1, 2, 2, 3, 3]
+    comms = C.init_all(devs, C.CommConfig(buffer_size=1 << 20, lanes=2))
+    try:
+        _log()
+        _allreduce_group(comms)
+        ev = _log()
+        launches = _check_launch_phase(ev, 4, 2, comms[0].nchannels * 2)
+        assert len(launches) == 4
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_two_stream_bridge_stays_on_each_device(fake):
+    """bridge_streams = 1 (libmccs user event -> comm stream -> backend event,
+    collectives.rs:86,134): every stream wait joins streams of one device."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20, bridge_streams=1))
+    try:
+        _log()
+        _allreduce_group(comms)
+        ev = _log()
+        _check_launch_phase(ev, 8, 1, comms[0].nchannels * comms[0].lanes)
+        assert sum(1 for k, _ in ev if k == "stream_wait") >= 8
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_external_launch_refuses_blocks_without_a_control_wave():
+    """mccs_hip_launch_coll: blocks of <= 64 threads have no control wave; the
+    argument check refuses them before any HIP call (no GPU needed)."""
+    lib = _lib.load()
+    f = lib.mccs_hip_launch_coll
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                  ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    invalid_argument, allreduce = 4, 4  # mccsInvalidArgument, mccsFuncAllReduce
+    assert f(allreduce, F32, SUM, 0x1000, 1, 0x2000, 1, 64, None) == invalid_argument
+    assert f(allreduce, F32, SUM, 0x1000, 1, 0x2000, 1, 608, None) == invalid_argument

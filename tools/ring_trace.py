@@ -18,7 +18,7 @@ from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-EV = {1: "ready", 2: "start", 3: "issued", 4: "drained", 5: "added", 6: "post"}
+EV = {1: "ready", 2: "start", 3: "issued", 4: "drained", 5: "added", 6: "post", 7: "enter", 8: "exit"}
 
 
 def main():
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--n", type=int, default=2)
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--mib", type=int, default=128)
+    ap.add_argument("--kib", type=int, default=0, help="bucket size in KiB (overrides --mib)")
     ap.add_argument("--show", type=int, default=12, help="slices printed per rank")
     args = ap.parse_args()
     lib = _lib.load()
@@ -39,7 +40,7 @@ def main():
     fn.restype = ctypes.c_int
     n = args.n
     comms = C.init_all([0] * n, C.CommConfig(lanes=args.lanes))
-    cnt = (args.mib << 20) // 4
+    cnt = ((args.kib << 10) if args.kib else (args.mib << 20)) // 4
     xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
     ys = [torch.empty_like(x) for x in xs]
 
@@ -52,20 +53,27 @@ def main():
         torch.cuda.synchronize()
 
     once()
-    buf = (ctypes.c_ulonglong * (2 << 15))()
-    fn(buf, 1 << 15)  # clear
+    R, W, S, E = 8, 10, 256, 9  # ring_kernel.h kTrace*
+    words = R * W * S * E
+    buf = (ctypes.c_ulonglong * words)()
+    assert fn(buf, words) == words  # clear
     once()
-    k = fn(buf, 1 << 15)
+    fn(buf, words)
+    import numpy as np
+
+    a = np.ctypeslib.as_array(buf).reshape(R, W, S, E)
+    nz = np.argwhere(a)
+    k = len(nz)
     ev = defaultdict(lambda: defaultdict(list))  # (rank) -> (t, ev) -> [(ts, wave)]
-    t0 = min(buf[2 * i] for i in range(k)) if k else 0
-    for i in range(k):
-        ts, w = buf[2 * i] - t0, buf[2 * i + 1]
-        e, wave, rank, t = w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFFFF, w >> 32
-        ev[rank][(t, EV[e])].append((ts, wave))
+    t0 = int(a[a > 0].min()) if k else 0
+    for rank, wave, t, e in nz:
+        ev[int(rank)][(int(t), EV[int(e)])].append((int(a[rank, wave, t, e]) - t0, int(wave)))
     rings = comms[0].rings()
     out = {"events": k, "n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels}
     print(json.dumps(out))
-    nsl = max(t for r in ev for (t, _) in ev[r]) + 1 if k else 0
+    for r in sorted(ev):
+        print(f"rank {r}: enter {min(x for x, _ in ev[r][(0, 'enter')])} exit {max(x for x, _ in ev[r][(0, 'exit')])}")
+    nsl = max(t for r in ev for (t, e) in ev[r] if e not in ("enter", "exit")) + 1 if k else 0
     lat, per = [], []
     for r in sorted(ev):
         prev = rings[0][(rings[0].index(r) - 1) % n]
