@@ -50,6 +50,15 @@ void default_rings(int n, int nch_req, std::vector<std::vector<int>>* rings) {
     std::vector<int> r(n);
     for (int i = 0; i < n; ++i) r[i] = i;
     base.push_back(r);
+  } else if (n == 8) {
+    // The complete symmetric digraph on 8 vertices splits into 7 arc-disjoint
+    // directed Hamiltonian cycles (Tillson 1980: K_n* does for every n except
+    // 4 and 6; these 7 were found by search and are checked arc-disjoint in
+    // tests/test_ring_host.py).  Every GPU then sends on all 7 of its xGMI
+    // links and receives on all 7, where both directions of 3 undirected
+    // cycles (the n != 8 construction below) leave one link per GPU idle.
+    base = {{0, 5, 6, 3, 7, 2, 1, 4}, {0, 4, 2, 3, 5, 7, 1, 6}, {0, 3, 2, 7, 5, 4, 6, 1}, {0, 7, 6, 2, 4, 1, 5, 3},
+            {0, 6, 7, 4, 3, 1, 2, 5}, {0, 2, 6, 5, 1, 3, 4, 7}, {0, 1, 7, 3, 6, 4, 5, 2}};
   } else if (n == 4) {
     // K4 has no two edge-disjoint Hamiltonian cycles; its three cycles cover
     // every edge exactly twice, so all six directed rings load links evenly.

@@ -15,9 +15,13 @@ Correctness gates (any failure exits non-zero, no line is printed):
   * after timing: the full-size exact-sum AllReduce again;
   * every extra leg (fp16 1 GiB, AllGather, size sweep, configs[4] jobs)
     validates its own results.
-A transport candidate is skipped only when its communicator cannot be
-created (e.g. IPC refuses to export that memory kind); a candidate that
-computes a wrong sum is a failure, not a fallback.
+A transport candidate is skipped when its communicator cannot be created
+(e.g. IPC refuses to export that memory kind) or when it fails the gate
+BEFORE timing (a wrong sum or a device watchdog in the uncached-FIFO mode on
+this node's xGMI): the next candidate (cached FIFOs + system-scope fences)
+is tried, and the rejection is recorded in config.rejected_before_timing.
+The mode that is timed must pass every gate; a failure after timing exits
+non-zero.
 """
 from __future__ import annotations
 
@@ -119,12 +123,25 @@ def _candidates(C, lanes_opts, locs):
     return out
 
 
-def make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, modes, full, group=None):
-    """Creates the communicator with the first mode whose init succeeds on
-    every rank, then gates it on exact-sum AllReduces (4 MiB fp32, and the
-    timed size and dtype).  Returns (comm, mode name) or (None, None) when
-    no mode could be created; a wrong sum raises BenchFailure."""
+def make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, modes, full, group=None,
+                        rejected=None, gate=None):
+    """Creates the communicator with the first mode that every rank can
+    create AND that passes the exact-sum gate on every rank (4 MiB fp32, and
+    the timed size and dtype).  A mode failing the gate is recorded in
+    `rejected` (list of dicts; its kind is skipped by later calls sharing the
+    list) and the next mode is tried.  Returns (comm, mode name), or
+    (None, None) when no mode passed.  `gate(comm) -> bool` replaces the
+    exact-sum gate (CPU tests of the agreement logic)."""
+    rejected = [] if rejected is None else rejected
+    if gate is None:
+        def gate(comm):
+            return (exact_sum_ok(torch, C, comm, rank, world, (4 << 20) // 4, torch.float32,
+                                 C.AllReduceDataType.Float32, dev)
+                    and exact_sum_ok(torch, C, comm, rank, world, full[0], full[1], full[2], dev))
     for name, cfg in modes:
+        kind = name.split("-", 1)[-1]  # e.g. "uncached-fifo"
+        if any(r["kind"] == kind for r in rejected):
+            continue
         try:
             comm = C.init_communicator_rank(rank, world, device, exchange, cfg)
         except Exception as e:  # noqa: BLE001  (e.g. IPC refuses this memory kind: try the next mode)
@@ -134,19 +151,26 @@ def make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, mode
             if comm is not None:
                 comm.destroy()
             continue
+        why = ""
         try:
-            ok = exact_sum_ok(torch, C, comm, rank, world, (4 << 20) // 4, torch.float32,
-                              C.AllReduceDataType.Float32, dev)
-            ok = ok and exact_sum_ok(torch, C, comm, rank, world, full[0], full[1], full[2], dev)
+            ok = bool(gate(comm))
+            why = "" if ok else "exact-sum mismatch"
         except Exception as e:  # noqa: BLE001  (watchdog / HIP error on this rank)
             print(f"[rank {rank}] {name}: {e}", flush=True)
-            ok = False
-        require(dist, ok, f"exact-sum AllReduce before timing ({name})", group)
-        return comm, name
+            ok, why = False, str(e)[:160]
+        if agree(dist, ok, group):
+            return comm, name
+        print(f"[rank {rank}] {name}: rejected before timing ({why or 'failed on another rank'})", flush=True)
+        rejected.append({"mode": name, "kind": kind, "rank0_reason": why if rank == 0 else None})
+        try:
+            comm.destroy()
+        except Exception as e:  # noqa: BLE001  (a comm that hit the watchdog may refuse a clean teardown)
+            print(f"[rank {rank}] {name}: destroy after rejection: {e}", flush=True)
     return None, None
 
 
-def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for, warmup=2, reps=6):
+def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for, warmup=2, reps=6,
+             ranks_share_gpu=False, rejected=None):
     """Transport placement chosen on the node itself: FIFO data at the
     receiver (remote writes) or at the sender (remote reads, the reference's
     SHM layout), each at the auto lane count and at 16 lanes per channel.
@@ -155,9 +179,12 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
     Returns (comm, mode, table)."""
     locs = [None] if "MCCS_LOCALITY" in os.environ else [C.LOCALITY_RECEIVER, C.LOCALITY_SENDER]
     lanes_opts = [None] if "MCCS_LANES" in os.environ else [None, 16]
+    if ranks_share_gpu and "MCCS_LANES" not in os.environ:
+        lanes_opts = [shared_gpu_lanes(world)]
     best, table, seen = None, [], set()
     for label, modes in _candidates(C, lanes_opts, locs):
-        comm, mode = make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, modes, full)
+        comm, mode = make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, modes, full,
+                                         rejected=rejected)
         if comm is None:
             table.append({"mode": label, "created": False})
             continue
@@ -175,8 +202,16 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
         else:
             comm.destroy()
     if best is None:
-        raise BenchFailure("no transport candidate could create a communicator")
+        raise BenchFailure("no transport candidate passed the exact-sum gate before timing")
     return best[1], best[2], table
+
+
+def shared_gpu_lanes(world: int) -> int:
+    """Lanes per channel when every rank is a process on ONE GPU (a 1-GPU
+    rehearsal): separate processes' ring kernels must all be resident at once
+    and the GPU does not guarantee that for many large grids (4 processes x
+    60 workgroups timed out on MI355X; 4 lanes ran), so keep them small."""
+    return 16 if world <= 2 else 4
 
 
 def graph_replay(torch, dist, comm, call_on, calls=10):
@@ -473,13 +508,17 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
         return lambda: C.all_reduce(cm, x, y, n, code, C.AllReduceOpType.Sum, stream)
 
     tune_table = None
+    share = ndev < world
+    rejected = []
     if getattr(args, "no_autotune", False):
+        lanes = shared_gpu_lanes(world) if share and "MCCS_LANES" not in os.environ else None
         comm, mode = make_validated_comm(torch, dist, C, rank, world, device, dev, exchange,
-                                         _candidates(C, [None], [None])[0][1], full)
+                                         _candidates(C, [lanes], [None])[0][1], full, rejected=rejected)
         if comm is None:
-            raise BenchFailure("communicator creation failed in every FIFO mode")
+            raise BenchFailure("no FIFO mode passed the exact-sum gate before timing")
     else:
-        comm, mode, tune_table = autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for)
+        comm, mode, tune_table = autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
+                                          ranks_share_gpu=share, rejected=rejected)
     K = args.steps
     C.ring_profile(device, reset=True)
     per_step = max_over_ranks(dist, time_steps(torch, dist, comm, step_for(comm), args.warmup, K)) / K
@@ -488,7 +527,7 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
     if os.environ.get("MCCS_BENCH_INJECT_MISMATCH") == "1":
         ok = False  # fault injection: the bench must exit non-zero
     require(dist, ok, "full-size exact-sum AllReduce after timing")
-    extras = {}
+    extras = {"rejected_before_timing": [{k: v for k, v in r.items() if v is not None} for r in rejected]}
     if not getattr(args, "no_extra", False):
         gr = graph_replay(torch, dist, comm, lambda st: C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, st))
         extras["graph_replay"] = {
@@ -520,7 +559,7 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
     prof = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()}
     return ring_line(world=world, steps=K, warmup=args.warmup, per_step_s=per_step, nbytes=nbytes, dt_name=dt_name,
                      comm_info=info, rings=rings, mode=mode, tune_table=tune_table, prof=prof,
-                     ranks_share_gpu=ndev < world, cpu_baseline=cpu, extras=extras)
+                     ranks_share_gpu=share, cpu_baseline=cpu, extras=extras)
 
 
 def setup2_jobs(world: int, interleaved: bool) -> list[list[int]]:
@@ -549,7 +588,9 @@ def setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup
     name, count = SETUP2_JOBS[job]
     nbytes, compute_us, _ = traffic.SETUP2[name]
     assert nbytes == 2 * count
-    modes = _candidates(C, [None], [None])[0][1]
+    share = torch.cuda.device_count() < world  # a 1-GPU rehearsal: every process on one GPU
+    modes = _candidates(C, [shared_gpu_lanes(world) if share and "MCCS_LANES" not in os.environ else None],
+                        [None])[0][1]
     comm, mode = make_validated_comm(torch, dist, C, jrank, half, device, dev, _exchange_factory(dist, half, grp),
                                      modes, (count, torch.float16, C.AllReduceDataType.Float16), grp)
     if comm is None:

@@ -122,3 +122,78 @@ def test_control_plane_world2(world):
         assert ok_ex and all_true and not one_false
         assert mx == world - 0.5
         assert ring_ok, f"rank {rank}: gloo ring != oracle"
+
+
+class _FakeComm:
+    def __init__(self, tag):
+        self.tag = tag
+        self.destroyed = False
+
+    def destroy(self):
+        self.destroyed = True
+
+
+class _FakeC:
+    """Stands in for mccs_amd.comm: creation joins the handle exchange like
+    the real init_communicator_rank, nothing else touches a device."""
+
+    def __init__(self):
+        self.made = []
+
+    def init_communicator_rank(self, rank, world, device, exchange, cfg):
+        exchange(b"h")
+        c = _FakeComm(cfg)
+        self.made.append(c)
+        return c
+
+
+def _gate_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from mccs_amd import ring_bench as rb
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        fc, rej = _FakeC(), []
+        ex = rb._exchange_factory(dist, world)
+
+        def gate(comm):  # rank 1 sees a wrong sum in every uncached-FIFO mode
+            return not (comm.tag == "U" and rank == 1)
+
+        m1 = [("receiver-uncached-fifo", "U"), ("receiver-cached-fifo+system-fences", "D")]
+        c1, n1 = rb.make_validated_comm(None, dist, fc, rank, world, 0, None, ex, m1, None,
+                                        rejected=rej, gate=gate)
+        m2 = [("sender-uncached-fifo", "U"), ("sender-cached-fifo+system-fences", "D")]
+        c2, n2 = rb.make_validated_comm(None, dist, fc, rank, world, 0, None, ex, m2, None, rejected=rej, gate=gate)
+        c3, n3 = rb.make_validated_comm(None, dist, fc, rank, world, 0, None, ex, m1, None, rejected=[],
+                                        gate=lambda c: False)
+        q.put((rank, n1, n2, n3, [r["kind"] for r in rej], len(fc.made), fc.made[0].destroyed,
+               c1.destroyed, c2.destroyed))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_gate_rejects_a_mode_on_every_rank_and_records_it():
+    """ring_bench.make_validated_comm: a mode that fails the exact-sum gate on
+    ANY rank is rejected on all ranks before timing (recorded, its FIFO kind
+    skipped afterwards), the next mode is chosen everywhere, and when every
+    mode fails no communicator is returned (the bench then exits non-zero)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_gate_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, n1, n2, n3, kinds, made, first_destroyed, c1_destroyed, c2_destroyed in res:
+        assert n1 == "receiver-cached-fifo+system-fences" and n2 == "sender-cached-fifo+system-fences"
+        assert n3 is None
+        assert kinds == ["uncached-fifo"]
+        # m1: U (rejected, destroyed) + D; m2: U skipped, D; m1 again with a fresh list: U + D both rejected
+        assert made == 5 and first_destroyed and not c1_destroyed and not c2_destroyed

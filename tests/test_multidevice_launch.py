@@ -79,7 +79,7 @@ def test_init_all_eight_devices_one_launch_per_device(fake):
         peers = {(int(kv["dev"]), int(kv["peer"])) for k, kv in ev if k == "peer"}
         assert peers == {(a, b) for a in range(8) for b in range(8) if a != b}
         lanes, nch = comms[0].lanes, comms[0].nchannels
-        assert nch == 6 and lanes == 10  # 3 edge-disjoint Hamiltonian cycles of K8, both directions
+        assert nch == 7 and lanes == 9  # 7 arc-disjoint directed Hamiltonian cycles: all 7 links per GPU
         _allreduce_group(comms)
         ev = _log()
         launches = _check_launch_phase(ev, 8, 1, nch * lanes)

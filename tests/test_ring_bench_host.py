@@ -36,7 +36,7 @@ def test_workload_labels():
 
 def _line(share, cpu=True):
     return rb.ring_line(world=8, steps=20, warmup=5, per_step_s=1.2e-3, nbytes=128 << 20, dt_name="float32",
-                        comm_info={"channels": 6, "lanes": 10, "block_threads": 512},
+                        comm_info={"channels": 7, "lanes": 9, "block_threads": 576},
                         rings=C.default_rings(8), mode="receiver-uncached-fifo", tune_table=[], prof={},
                         ranks_share_gpu=share,
                         cpu_baseline=rb.cpu_sum_baseline(2, 1 << 20, budget_s=0.2) if cpu else None)
@@ -60,7 +60,7 @@ def test_ring_line_schema(share):
     if share:
         assert rf["peak"] == 8000.0 and abs(rf["achieved"] - 44 * (128 << 20) / 1.2e-3 / 1e9) < 0.01
     else:
-        assert rf["peak"] == 6 * rb.XGMI_LINK_GBPS_PER_DIR
+        assert rf["peak"] == 7 * rb.XGMI_LINK_GBPS_PER_DIR  # all 7 links (7 directed rings)
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
     assert cb["host"]["affinity_threads"] >= 1 and "nproc" in cb["host"]

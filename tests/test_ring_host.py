@@ -41,9 +41,17 @@ def test_default_rings_edge_disjoint(n):
     assert len(rings) >= n - 2  # K_n: floor((n-1)/2) Hamiltonian cycles x 2 directions
 
 
-def test_n8_uses_six_links():
+def test_n8_uses_all_seven_links_both_ways():
+    """n = 8: 7 arc-disjoint directed Hamiltonian cycles cover all 56 arcs of
+    the complete digraph, so every GPU sends and receives on all 7 xGMI links,
+    one ring per link and direction."""
     rings = comm.default_rings(8)
-    assert len(rings) == 6
+    assert len(rings) == 7
+    use = Counter((r[i], r[(i + 1) % 8]) for r in rings for i in range(8))
+    assert len(use) == 56 and set(use.values()) == {1}
+    for g in range(8):
+        assert {b for (a, b) in use if a == g} == set(range(8)) - {g}
+        assert {a for (a, b) in use if b == g} == set(range(8)) - {g}
 
 
 def test_n4_balanced_overlap():
