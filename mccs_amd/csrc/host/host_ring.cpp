@@ -5,12 +5,16 @@
 // Same protocol as the gfx950 kernels (ring.hip) and the reference
 // (all_reduce.h:10-87 schedule; prims_simple.h:68-237 FIFO: 8 slots, slices of
 // 2 steps, sender waits head + 8 >= step + 2, receiver waits tail >= step + 2,
-// operand order fn(own input, received)), with one std::thread per
-// (rank, channel) and std::atomic head/tail counters.  It exists so the FIFO
+// operand order fn(own input, received)), with one host thread per
+// (rank, channel) and std::atomic head/tail counters.  The threads and the
+// FIFOs persist across calls (HostRingPool): a call hands each task to its
+// own parked worker, so a 1 KiB AllReduce costs no thread creation.  It exists so the FIFO
 // protocol and schedule can be exercised end to end without a GPU; it is not
 // a fallback for the device path (nothing on the device path calls it).
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -179,9 +183,16 @@ void run_rank_channel(Ctx* c, int rank, int ch) {
   const char* input = (const char*)c->send[rank];
   char* output = (char*)c->recv[rank];
   uint64_t rstep = 0, sstep = 0;
-  std::unique_ptr<char[]> tmp(new char[(size_t)(2 * stepSize * c->es)]);
+  thread_local std::vector<char> tmp_store;  // this worker's staging slice, kept across calls
+  if (tmp_store.size() < (size_t)(2 * stepSize * c->es)) tmp_store.resize((size_t)(2 * stepSize * c->es));
+  char* const tmp = tmp_store.data();
   const auto t0 = std::chrono::steady_clock::now();
   auto wait_geq = [&](std::atomic<uint64_t>& f, uint64_t target) {
+    // the peer is a running thread: spin (pause) before giving up the core
+    for (int spin = 0; spin < 4096; ++spin) {
+      if (f.load(std::memory_order_acquire) >= target) return true;
+      __builtin_ia32_pause();
+    }
     while (f.load(std::memory_order_acquire) < target) {
       if (c->failed.load(std::memory_order_relaxed)) return false;
       if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
@@ -210,11 +221,11 @@ void run_rank_channel(Ctx* c, int rank, int ch) {
       char* sslot = out.data.get() + (sstep % 8) * stepSize * c->es;
       if (bytes) {
         // vals = srcs[0]; vals = fn(vals, srcs[1]) with srcs = [input?, recv?]
-        if (SRC && RECV) apply(c->dt, c->op, tmp.get(), input + (srcIx + offset) * c->es, rslot, (size_t)real);
-        else if (SRC) std::memcpy(tmp.get(), input + (srcIx + offset) * c->es, bytes);
-        else std::memcpy(tmp.get(), rslot, bytes);
-        if (DST) std::memcpy(output + (dstIx + offset) * c->es, tmp.get(), bytes);
-        if (SEND) std::memcpy(sslot, tmp.get(), bytes);
+        if (SRC && RECV) apply(c->dt, c->op, tmp, input + (srcIx + offset) * c->es, rslot, (size_t)real);
+        else if (SRC) std::memcpy(tmp, input + (srcIx + offset) * c->es, bytes);
+        else std::memcpy(tmp, rslot, bytes);
+        if (DST) std::memcpy(output + (dstIx + offset) * c->es, tmp, bytes);
+        if (SEND) std::memcpy(sslot, tmp, bytes);
       }
       if (SEND) out.tail.store(sstep + 2, std::memory_order_release);
       if (RECV) in.head.store(rstep + 2, std::memory_order_release);
@@ -248,6 +259,90 @@ void run_rank_channel(Ctx* c, int rank, int ch) {
   }
 }
 
+// Parked worker threads, one per concurrent (rank, channel) task: every task
+// of a call must run at the same time (they spin on each other's FIFO flags),
+// so task i always goes to worker i.  Workers spin briefly after a call (back
+// to back calls wake them in ~1 us) and then sleep on a condition variable.
+class HostRingPool {
+ public:
+  static HostRingPool& get() {
+    static HostRingPool* p = new HostRingPool();  // never destroyed: workers stay parked at exit
+    return *p;
+  }
+  std::mutex call_mu;
+
+  // FIFOs of `nconn` connectors of `bytes` each, counters reset
+  std::vector<HostConn>& fifos(size_t nconn, size_t bytes) {
+    if (conns_.size() != nconn || conn_bytes_ != bytes) {
+      conns_ = std::vector<HostConn>(nconn);
+      for (auto& hc : conns_) hc.data.reset(new char[bytes]);
+      conn_bytes_ = bytes;
+    }
+    for (auto& hc : conns_) {
+      hc.head.store(0, std::memory_order_relaxed);
+      hc.tail.store(0, std::memory_order_relaxed);
+    }
+    return conns_;
+  }
+
+  void run(Ctx* c, int ntasks) {
+    while ((int)workers_.size() < ntasks) {
+      const int id = (int)workers_.size();
+      workers_.emplace_back([this, id] { loop(id); });
+    }
+    remaining_.store(ntasks, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = c;
+      ntasks_ = ntasks;
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    for (int spin = 0; remaining_.load(std::memory_order_acquire) != 0; ++spin) {
+      if (spin < 4096) __builtin_ia32_pause();
+      else std::this_thread::yield();
+    }
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      // spin ~200 us for the next call, then sleep
+      const auto t0 = std::chrono::steady_clock::now();
+      while (gen_.load(std::memory_order_acquire) == seen &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+        __builtin_ia32_pause();
+      if (gen_.load(std::memory_order_acquire) == seen) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+      }
+      Ctx* c;
+      int ntasks;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        seen = gen_.load(std::memory_order_acquire);
+        c = job_;
+        ntasks = ntasks_;
+      }
+      if (id < ntasks) {
+        run_rank_channel(c, id / c->nch, id % c->nch);
+        remaining_.fetch_sub(1, std::memory_order_acq_rel);
+      }
+    }
+  }
+
+  std::vector<std::thread> workers_;
+  std::vector<HostConn> conns_;
+  size_t conn_bytes_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> remaining_{0};
+  Ctx* job_ = nullptr;
+  int ntasks_ = 0;
+};
+
 }  // namespace
 
 extern "C" mccsResult_t mccs_host_ring_allreduce(int nranks, const void* const* sendbufs, void* const* recvbufs,
@@ -262,8 +357,9 @@ extern "C" mccsResult_t mccs_host_ring_allreduce(int nranks, const void* const* 
     if (recvbufs[0] != sendbufs[0]) std::memmove(recvbufs[0], sendbufs[0], count * es);
     return mccsSuccess;
   }
-  std::vector<HostConn> conns((size_t)nchannels * nranks);
-  for (auto& hc : conns) hc.data.reset(new char[(size_t)buff_size]);
+  HostRingPool& pool = HostRingPool::get();
+  std::lock_guard<std::mutex> call(pool.call_mu);  // one host-ring AllReduce at a time
+  std::vector<HostConn>& conns = pool.fifos((size_t)nchannels * nranks, (size_t)buff_size);
   Ctx c;
   c.n = nranks;
   c.nch = nchannels;
@@ -278,9 +374,6 @@ extern "C" mccsResult_t mccs_host_ring_allreduce(int nranks, const void* const* 
   c.rings = rings;
   c.conns = &conns;
   c.timeout_s = 60.0;
-  std::vector<std::thread> th;
-  for (int r = 0; r < nranks; ++r)
-    for (int ch = 0; ch < nchannels; ++ch) th.emplace_back(run_rank_channel, &c, r, ch);
-  for (auto& t : th) t.join();
+  pool.run(&c, nranks * nchannels);
   return c.failed.load() ? mccsTimeout : mccsSuccess;
 }
