@@ -397,6 +397,32 @@ def cpu_sum_baseline(world: int, nbytes: int, budget_s: float = 6.0) -> dict:
             "single_thread_value": round(res["st"][0], 3), "host": host_record()}
 
 
+def cpu_ring_baseline(world: int, nbytes: int, nchannels: int, budget_s: float = 4.0) -> dict:
+    """SURVEY §8(d) configs[2]: the same ring schedule run by host threads
+    over host memory (mccs_host_ring_allreduce: `world` ranks x `nchannels`
+    threads, FIFOs in shared memory), on a bounded sample of the bucket.
+    value = sample bytes / t (algbw, as the GPU line)."""
+    import numpy as np
+
+    from mccs_amd import comm as C
+
+    n = nbytes // 4
+    rng = np.random.default_rng(0x6D636373)
+    send = [(rng.random(n, dtype=np.float32) * 2 - 1) for _ in range(world)]
+    recv = [np.empty_like(x) for x in send]
+    C.host_ring_allreduce(send, recv, n, C.AllReduceDataType.Float32, channels=nchannels, nthreads=544)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        C.host_ring_allreduce(send, recv, n, C.AllReduceDataType.Float32, channels=nchannels, nthreads=544)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or reps >= 200:
+            break
+    return {"value": round(nbytes * reps / el / 1e9, 3), "unit": "GB/s algbw (S/t)", "threads": world * nchannels,
+            "kind": "port", "sample": f"{world} ranks x {nbytes >> 20} MiB fp32, {nchannels} channels, host-thread "
+                                      f"ring (same schedule and FIFO protocol), {reps} AllReduces in {el:.2f}s"}
+
+
 def ring_roofline(world, nbytes, per_step_s, links, ranks_share_gpu, kernel):
     """Bound of one rank's ring AllReduce.  On a node: the xGMI links the rank
     sends on, per-rank link bytes 2(n-1)/n*S.  When every rank shares one
@@ -555,6 +581,7 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
     cpu = None
     if not getattr(args, "no_cpu_baseline", False):
         cpu = cpu_sum_baseline(world, nbytes)
+        extras["cpu_ring_baseline"] = cpu_ring_baseline(world, min(nbytes, 16 << 20), info["channels"])
     dist.barrier()
     prof = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()}
     return ring_line(world=world, steps=K, warmup=args.warmup, per_step_s=per_step, nbytes=nbytes, dt_name=dt_name,
