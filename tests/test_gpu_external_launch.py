@@ -1,0 +1,67 @@
+"""mccs_hip_launch_coll (the external-planner launch, plan.rs:638-669) with two
+ranks of ONE GPU in ONE process: the second rank's launch is refused while the
+first is still running (the two kernels spin on each other's flags, so
+separate launches of co-located ranks would deadlock until the watchdog).
+The running kernel is then ended through its abortFlag (mccsCommAbort)."""
+import ctypes
+import time
+
+import numpy as np
+import pytest
+
+from mccs_amd import _lib
+from mccs_amd import abi
+from mccs_amd import comm as C
+
+pytestmark = pytest.mark.gpu
+
+FUNC_ALLREDUCE, F32 = 4, 7
+INVALID_USAGE = 5  # mccsInvalidUsage
+
+
+def _works(nch, send, recv, count, nthr):
+    works = (abi.mccsDevWork * nch)()
+    for c in range(nch):
+        w = works[c]
+        e = w.elems[0]
+        e.isUsed, e.nWarps = 1, nthr // 32
+        e.sendbuff, e.recvbuff, e.count = send, recv, count
+        e.bid, e.nChannels = c, nch
+        w.header.type = 1  # mccsDevWorkTypeColl
+        w.header.isLast, w.header.inFifo, w.header.doneAcks = 1, 0, 0
+    return works
+
+
+def test_colocated_external_launch_refused_while_peer_runs():
+    import torch
+
+    lib = _lib.load()
+    f = lib.mccs_hip_launch_coll
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                  ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    comms = C.init_all([0, 0], C.CommConfig(lanes=1, timeout_ms=20000))
+    try:
+        nch, nthr, count = comms[0].nchannels, 544, 1 << 20
+        xs = [torch.ones(count, device="cuda") for _ in range(2)]
+        ys = [torch.zeros(count, device="cuda") for _ in range(2)]
+        wbufs = [torch.frombuffer(bytearray(bytes(_works(nch, xs[r].data_ptr(), ys[r].data_ptr(), count, nthr))),
+                                  dtype=torch.uint8).cuda() for r in range(2)]
+        st = torch.cuda.Stream()  # non-blocking: the abort below must not wait for the kernel
+        torch.cuda.synchronize()
+        rc0 = f(FUNC_ALLREDUCE, F32, 0, comms[0].dev_comm(), (1 << nch) - 1, wbufs[0].data_ptr(), nch, nthr,
+                st.cuda_stream)
+        assert rc0 == 0
+        time.sleep(0.05)  # rank 0 now spins on rank 1's flags
+        rc1 = f(FUNC_ALLREDUCE, F32, 0, comms[1].dev_comm(), (1 << nch) - 1, wbufs[1].data_ptr(), nch, nthr,
+                st.cuda_stream)
+        assert rc1 == INVALID_USAGE, rc1
+        comms[0].abort()  # raises rank 0's abortFlag: its control waves end the kernel
+        t0 = time.perf_counter()
+        st.synchronize()
+        assert time.perf_counter() - t0 < 10, "the aborted kernel did not end promptly"
+        assert np.all(ys[0].cpu().numpy() != 2.0)  # never completed: no peer
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
