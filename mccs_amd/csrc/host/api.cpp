@@ -336,11 +336,12 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
   DeviceGuard g(c->device);
   MCCS_HIP(rt().EventSynchronize(c->event));
   if (c->stream) MCCS_HIP(rt().StreamSynchronize(c->stream));
-  unsigned err = 0;
-  MCCS_HIP(rt().TakeDeviceError(&err, c->launched_tus));
-  c->launched_tus = 0;
-  uint32_t abort_val = 0;
-  MCCS_HIP(rt().Memcpy(&abort_val, c->d_abort, sizeof(abort_val), hipMemcpyDeviceToHost));
+  // the communicator's abort line: word 0 abortFlag, word 1 the error bits its
+  // kernels reported (ring_cfg.h), so another communicator's failure never
+  // shows up here
+  uint32_t line[2] = {0, 0};
+  MCCS_HIP(rt().Memcpy(line, c->d_abort, sizeof(line), hipMemcpyDeviceToHost));
+  const uint32_t abort_val = line[0], err = line[1];
   if (err || abort_val) c->failed = true;
   if (err & MCCS_ERR_TIMEOUT) return mccsTimeout;
   if (err || abort_val) return mccsRemoteError;

@@ -94,6 +94,7 @@ void default_rings(int n, int nch_req, std::vector<std::vector<int>>* rings) {
 mccsResult_t comm_set_kernel_cfg(Comm* c) {
   mccsRingKernelCfg k{};
   k.fence_mode = c->all_uncached ? MCCS_FENCE_UNCACHED : MCCS_FENCE_SYSTEM;
+  k.err_line = 1;  // d_abort is a 64-byte line of ours: errors go to its word 1
   const int tmo = c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms;
   k.timeout_ticks = tmo < 0 ? 0 : (uint64_t)tmo * 100000ull;  // s_memrealtime: 100 MHz
   // one 4-step slice per chunk (2 slices in flight per lane): one flag

@@ -149,7 +149,6 @@ struct Comm {
   // plan state
   std::vector<ChannelSchedule> sched;
   int plan_func = -1, plan_dtype = -1, plan_op = -1, plan_threads = 0;
-  unsigned launched_tus = 0;  // ring translation units launched since the last mccsCommSync
   bool plan_pending = false;
 };
 
@@ -169,10 +168,6 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
 const void* ring_kernel_ptr(int func, int dtype, int op);
 const void* ring_multi_kernel_ptr(int func, int dtype, int op);
 int coresident_ring_blocks(int block, int device);
-// ORs (and clears) the device error words of the ring translation units in
-// `tu_mask` (bit ring_tu_index(func, op) per kind of kernel launched).
-hipError_t ring_take_device_error(unsigned* err, unsigned tu_mask);
-int ring_tu_index(int func, int op);
 hipError_t ring_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_flush_caches(hipStream_t st);
 

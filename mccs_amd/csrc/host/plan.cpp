@@ -334,7 +334,6 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
           ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps)
         return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
       ma.comm[k] = (mccsDevComm*)ck->d_comm;
-      comms[idx[k]]->launched_tus |= 1u << ring_tu_index(ck->plan_func, ck->plan_op);
       ma.work[k] = lds[k].work;
       if (ck->kcfg.fence_mode != MCCS_FENCE_UNCACHED) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
       ma.cfg.timeout_ticks = (ma.cfg.timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)

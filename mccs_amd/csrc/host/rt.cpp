@@ -77,7 +77,6 @@ class HipRuntime final : public DeviceRuntime {
   hipError_t CuCount(int* ncu, int device) override {
     return hipDeviceGetAttribute(ncu, hipDeviceAttributeMultiprocessorCount, device);
   }
-  hipError_t TakeDeviceError(unsigned* err, unsigned tu_mask) override { return ring_take_device_error(err, tu_mask); }
 };
 
 // Recording fake: "device" memory is host memory tagged with its device,
@@ -217,11 +216,6 @@ class FakeRuntime final : public DeviceRuntime {
   }
   hipError_t CuCount(int* ncu, int) override {
     *ncu = 256;
-    return hipSuccess;
-  }
-  hipError_t TakeDeviceError(unsigned* err, unsigned) override {
-    *err = 0;
-    note("host_wait what=error dev=" + std::to_string(cur_));
     return hipSuccess;
   }
 

@@ -46,7 +46,6 @@ class DeviceRuntime {
   virtual hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) = 0;
   virtual hipError_t BlocksPerCu(int* per_cu, const void* fn, int block) = 0;
   virtual hipError_t CuCount(int* ncu, int device) = 0;
-  virtual hipError_t TakeDeviceError(unsigned* err, unsigned tu_mask) = 0;
 };
 
 DeviceRuntime& rt();

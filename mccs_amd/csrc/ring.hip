@@ -26,10 +26,6 @@ hipError_t ring_tu_ar_sum_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_tu_ar_prod_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_tu_ar_max_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_tu_ar_min_read_profile(unsigned long long* out, bool reset);
-hipError_t ring_tu_ar_sum_take_error(unsigned* err);
-hipError_t ring_tu_ar_prod_take_error(unsigned* err);
-hipError_t ring_tu_ar_max_take_error(unsigned* err);
-hipError_t ring_tu_ar_min_take_error(unsigned* err);
 
 static const void* ar_kernel(int dtype, int op, bool multi) {
   if (dtype < 0 || dtype >= mccsNumTypes) return nullptr;
@@ -79,24 +75,6 @@ hipError_t ring_read_profile(unsigned long long* out, bool reset) {
       ring_tu_ar_max_read_profile, ring_tu_ar_min_read_profile};
   for (auto rd : readers) {
     hipError_t e = rd(out, reset);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-
-// Translation unit of a collective's kernels: 0 AllGather, 1 + op AllReduce.
-int ring_tu_index(int func, int op) { return func == mccsFuncAllGather ? 0 : 1 + (op & 3); }
-
-// ORs (and clears) the device error words of the ring translation units in
-// tu_mask: one device read per kind of kernel a communicator launched.
-hipError_t ring_take_device_error(unsigned* err, unsigned tu_mask) {
-  *err = 0;
-  hipError_t (*const takers[])(unsigned*) = {ring_tu_ag_take_error, ring_tu_ar_sum_take_error,
-                                             ring_tu_ar_prod_take_error, ring_tu_ar_max_take_error,
-                                             ring_tu_ar_min_take_error};
-  for (int i = 0; i < 5; ++i) {
-    if (!(tu_mask >> i & 1)) continue;
-    hipError_t e = takers[i](err);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -27,7 +27,10 @@
 #define MCCS_FENCE_SYSTEM 0   // FIFO memory may be cached: system-scope release/acquire
 #define MCCS_FENCE_UNCACHED 1 // FIFO memory is uncached (hipDeviceMallocUncached): drains only
 
-// Error bits reported through the device-global error word.
+// Error bits a ring kernel reports for ONE communicator: word 1 of the
+// communicator's own abort line (abortFlag[1]; the library allocates that line,
+// 64 bytes, zeroed at init), read back by mccsCommSync.  A process-wide word
+// would let one communicator's abort fail another's sync.
 #define MCCS_ERR_TIMEOUT 1u
 #define MCCS_ERR_ABORTED 2u
 
@@ -36,7 +39,10 @@ struct mccsRingKernelCfg {
   uint32_t slice_steps;   // FIFO steps per slice: 2 (reference SliceSteps) or 4 (one slice per chunk)
   uint64_t timeout_ticks; // s_memrealtime ticks (100 MHz); 0 = never
   uint32_t profile;       // 1: accumulate per-slice wait / work ticks (mccs_ring_profile)
-  uint32_t pad2;
+  uint32_t err_line;      // 1: error bits go to abortFlag[1] (library launches: the abort line is
+                          // ours); 0: reference-named kernels, whose abortFlag is the caller's
+                          // 4-byte allocation: only abortFlag itself is raised (the reference's
+                          // one error channel, devcomm.h abortFlag)
 };
 
 // Per-device ring profile counters (s_memrealtime ticks, 100 MHz), summed

@@ -61,7 +61,20 @@ def test_colocated_external_launch_refused_while_peer_runs():
         st.synchronize()
         assert time.perf_counter() - t0 < 10, "the aborted kernel did not end promptly"
         assert np.all(ys[0].cpu().numpy() != 2.0)  # never completed: no peer
+        with pytest.raises(_lib.MccsError):
+            comms[0].sync()  # the aborted communicator reports its failure ...
     finally:
         torch.cuda.synchronize()
         for c in comms:
             c.destroy()
+    # ... and only that one: error bits live in each communicator's own abort
+    # line, so a fresh communicator in the same process syncs clean (a
+    # process-wide error word once failed the next test's first AllReduce)
+    import vnode
+
+    fresh = C.init_all([0, 0])
+    try:
+        outs = vnode.run_allreduce(fresh, [np.ones(4096, np.float32)] * 2, F32, 0)
+        assert all(np.all(o == 2.0) for o in outs)
+    finally:
+        vnode.destroy(fresh)
