@@ -18,7 +18,8 @@ from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-EV = {1: "ready", 2: "start", 3: "issued", 4: "drained", 5: "added", 6: "post", 7: "enter", 8: "exit"}
+EV = {1: "ready", 2: "start", 3: "issued", 4: "drained", 5: "added", 6: "post", 7: "enter", 8: "exit",
+      9: "loaded", 10: "conn"}
 
 
 def main():
@@ -53,7 +54,7 @@ def main():
         torch.cuda.synchronize()
 
     once()
-    R, W, S, E = 8, 10, 256, 9  # ring_kernel.h kTrace*
+    R, W, S, E = 8, 10, 256, 11  # ring_kernel.h kTrace*
     words = R * W * S * E
     buf = (ctypes.c_ulonglong * words)()
     assert fn(buf, words) == words  # clear
@@ -72,8 +73,10 @@ def main():
     out = {"events": k, "n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels}
     print(json.dumps(out))
     for r in sorted(ev):
-        print(f"rank {r}: enter {min(x for x, _ in ev[r][(0, 'enter')])} exit {max(x for x, _ in ev[r][(0, 'exit')])}")
-    nsl = max(t for r in ev for (t, e) in ev[r] if e not in ("enter", "exit")) + 1 if k else 0
+        first = {e: min((x for x, _ in ev[r].get((0, e), [])), default=None) for e in ("enter", "loaded", "conn")}
+        print(f"rank {r}: enter {first['enter']} loaded {first['loaded']} conn {first['conn']} "
+              f"exit {max(x for x, _ in ev[r][(0, 'exit')])}")
+    nsl = max(t for r in ev for (t, e) in ev[r] if e not in ("enter", "exit", "loaded", "conn")) + 1 if k else 0
     lat, per = [], []
     for r in sorted(ev):
         prev = rings[0][(rings[0].index(r) - 1) % n]

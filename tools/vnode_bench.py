@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--sizes-mib", type=int, nargs="+", default=[1, 16, 128])
+    ap.add_argument("--sizes-kib", type=int, nargs="+", default=None, help="bucket sizes in KiB (override MiB)")
     ap.add_argument("--lanes", type=int, nargs="+", default=[0])
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
@@ -35,8 +36,8 @@ def main():
         for lanes in args.lanes:
             comms = C.init_all([0] * n, C.CommConfig(lanes=lanes, block_threads=args.block,
                                                           bridge_streams=args.bridge or None))
-            for mib in args.sizes_mib:
-                cnt = (mib << 20) // 4
+            for kib in (args.sizes_kib or [m << 10 for m in args.sizes_mib]):
+                cnt = (kib << 10) // 4
                 xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
                 ys = [torch.empty_like(x) for x in xs]
 
@@ -77,10 +78,10 @@ def main():
                     graph_ms = (time.perf_counter() - t0) / args.iters * 1e3
                     del g
                 print(json.dumps({"n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels,
-                                  "block": comms[0].block_threads, "bridge": args.bridge, "MiB": mib, "ms": round(dt * 1e3, 3),
-                                  "algbw_GBps": round((mib << 20) / dt / 1e9, 2), "slice_profile": prof,
+                                  "block": comms[0].block_threads, "bridge": args.bridge, "KiB": kib, "ms": round(dt * 1e3, 4),
+                                  "algbw_GBps": round((kib << 10) / dt / 1e9, 2), "slice_profile": prof,
                                   "graph_ms": round(graph_ms, 4) if graph_ms else None,
-                                  "graph_algbw_GBps": round((mib << 20) / graph_ms / 1e6, 2) if graph_ms else None}),
+                                  "graph_algbw_GBps": round((kib << 10) / graph_ms / 1e6, 2) if graph_ms else None}),
                       flush=True)
                 del xs, ys
             torch.cuda.synchronize()
