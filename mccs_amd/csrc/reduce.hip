@@ -178,6 +178,21 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_wave_base)
 #undef MCCS_GLDS
 }
 
+#ifdef MCCS_REDUCE_TRACE
+// A/B builds only (tools/reduce_skew.py): per wave of the latest launch,
+// {entry, exit} s_memrealtime and the XCC the wave ran on.
+constexpr int kRTraceWaves = 8192;
+__device__ unsigned long long g_rtrace[kRTraceWaves * 3];
+__device__ __forceinline__ void rtrace(int gw, int k) {
+  if ((threadIdx.x & 63) != 0 || gw >= kRTraceWaves) return;
+  g_rtrace[gw * 3 + k] = __builtin_amdgcn_s_memrealtime();
+  if (k == 1) g_rtrace[gw * 3 + 2] = __builtin_amdgcn_s_getreg((20 /* HW_REG_XCC_ID */) | (0 << 6) | (15 << 11)) & 15;
+}
+#define MCCS_RTRACE(gw, k) rtrace((int)(gw), k)
+#else
+#define MCCS_RTRACE(gw, k) ((void)0)
+#endif
+
 template <int DT, int OP, int U, int S, int W, int LDP, int STP>
 __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
   constexpr int PACK = kPackElems<DT>;
@@ -196,6 +211,7 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
   const u32x4* s0 = (const u32x4*)a.srcs[0];
   const u32x4* s1 = (const u32x4*)a.srcs[1];
   u32x4* d0 = (u32x4*)a.dsts[0];
+  MCCS_RTRACE(gw, 0);
 
   auto issue = [&](int64_t tile, int stage) {
     const uint32_t base = wave_lds + (uint32_t)(stage * STAGE_BYTES);
@@ -239,6 +255,7 @@ __global__ void __launch_bounds__(W * 64) reduce_lds_kernel(ReduceArgs a) {
       st16<STP>(d0 + p, pack_op<DT, OP>(x, y));
     }
   }
+  MCCS_RTRACE(gw, 1);
   if (blockIdx.x == gridDim.x - 1) {
     using T = typename Elem<DT>::T;
     for (int64_t e = npack * PACK + threadIdx.x; e < a.count; e += W * 64) {
@@ -519,6 +536,14 @@ extern "C" void mccs_hip_reduce_get_tune(int* variant, int* unroll, int* policy,
   if (stages) *stages = g_tune.stages;
   if (waves) *waves = g_tune.waves;
 }
+
+#ifdef MCCS_REDUCE_TRACE
+extern "C" int mccs_reduce_trace(unsigned long long* out, int max_words) {
+  if (max_words < kRTraceWaves * 3) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rtrace), sizeof(g_rtrace), 0, hipMemcpyDeviceToHost)) return -1;
+  return kRTraceWaves * 3;
+}
+#endif
 
 extern "C" mccsResult_t mccs_hip_reduce_tune_grid(int blocks) {
   if (blocks < 0) return mccsInvalidArgument;
