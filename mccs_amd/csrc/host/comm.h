@@ -62,7 +62,7 @@ struct DeviceGuard {
 struct ArenaLayout {
   int nch = 0;
   size_t buffer_size = 0;
-  static constexpr size_t kLinesBytes = (size_t)MCCS_MAX_LANES * MCCS_FLAG_LINE_BYTES;  // 2 KiB
+  static constexpr size_t kLinesBytes = (size_t)MCCS_MAX_LANES * MCCS_FLAG_LINE_BYTES;  // 8 KiB
   size_t head_off(int c) const { return (size_t)c * 2 * kLinesBytes; }
   size_t tail_off(int c) const { return (size_t)c * 2 * kLinesBytes + kLinesBytes; }
   size_t flags_bytes() const { return (((size_t)nch * 2 * kLinesBytes) + 65535) & ~(size_t)65535; }

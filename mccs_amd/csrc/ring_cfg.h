@@ -13,7 +13,7 @@
 
 #define MCCS_FLAG_LINE_BYTES 128
 #define MCCS_FLAG_LINE_WORDS (MCCS_FLAG_LINE_BYTES / 8)
-#define MCCS_MAX_LANES 16
+#define MCCS_MAX_LANES 64
 // Largest ring workgroup.  576 = 9 waves covers the reference's 17-warp (544
 // thread) blocks (get_task_schema, plan.rs:602-635) and keeps ~168 VGPRs per
 // lane (3 waves per SIMD): the fully inlined ring loop with 8 packs in flight

@@ -206,6 +206,24 @@ def test_configs(orc, cfg):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("lanes", [33, 64])
+@pytest.mark.parametrize("count", [5000, 777777, (37 << 20) // 4 + 3])
+def test_wide_lanes(orc, lanes, count):
+    """Up to MCCS_MAX_LANES = 64 workgroups per channel (a 2-rank virtual node
+    then fills every CU): each lane owns a fixed 256-byte-aligned region of a
+    slot group, 32 KiB at 64 lanes; bit-exact, multi-loop sizes included."""
+    n = 2
+    comms = C.init_all([0] * n, C.CommConfig(lanes=lanes))
+    try:
+        rng = np.random.default_rng(lanes + count)
+        inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, F32, 0)
+        exp = vnode.expected_allreduce(orc, inputs, F32, 0, comms[0])
+        _check_all_equal(outs, exp, F32)
+    finally:
+        vnode.destroy(comms)
+
+
 def test_single_rank_is_copy():
     import torch
 
