@@ -109,7 +109,7 @@ typedef struct mccsComm *mccsComm_t;
 typedef struct {
   int channel_count;    /* rings; 0 = auto: 2 x edge-disjoint Hamiltonian cycles of the node */
   int buffer_size;      /* FIFO bytes per connection (buffer_sizes[0]); 0 = 4 MiB */
-  int lanes;            /* workgroups per channel; 0 = auto (64 / channels, <= 16, fitted to residency) */
+  int lanes;            /* workgroups per channel; 0 = auto (64 / channels, <= 64, fitted to residency) */
   int block_threads;    /* threads per workgroup (64..576, multiple of 32); 0 = 512 */
   int locality;         /* MCCS_LOCALITY_*; default RECEIVER (remote writes; SENDER = reference shm layout) */
   int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED */
@@ -117,6 +117,10 @@ typedef struct {
   int work_fifo_depth;  /* mccsDevWork slots (power of two); 0 = 4096 */
   int bridge_streams;   /* -1 (default): launch on the caller's stream; 1: user stream -> comm stream -> user stream events (libmccs two-stream bridge) */
   const int *rings;     /* channel_count x nranks send orders (comm_patterns_override); NULL = auto */
+  int fifo_slots;       /* FIFO slots per connection of buffer_size / 8 bytes each: 8 (the reference's
+                           MCCS_BUFFER_SLOTS), 16 or 32; 0 = default (16).  More slots = more slices in
+                           flight per lane; the chunk schedule (and so every result) still follows
+                           buffer_size, as in the reference */
 } mccsCommConfig;
 
 void mccsCommConfigDefault(mccsCommConfig *cfg);

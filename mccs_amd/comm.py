@@ -78,6 +78,7 @@ class CommConfig:
     work_fifo_depth: int | None = None
     bridge_streams: int | None = None
     rings: list | None = None  # comm_patterns_override: channel_count x nranks send orders
+    fifo_slots: int | None = None  # FIFO slots per connection: 8 (reference), 16, 32
 
     def to_c(self, nranks: int):
         c = _CommConfig()

@@ -43,6 +43,11 @@ static void fill_defaults(mccsCommConfig* c) {
   // user-event -> comm-stream -> backend-event bridge, without the ~10 us per
   // cross-stream wait measured on MI355X); 1 keeps the two-stream bridge
   if (c->bridge_streams == 0) c->bridge_streams = -1;
+  // 16 slots: four 4-step slices in flight per lane instead of two (n = 8
+  // virtual node +5 % at 128 MiB, +10 % at 16 MiB; n = 2 / 4 unchanged), more
+  // bytes in flight per lane to cover an xGMI hop; 2 x the FIFO memory
+  // (8 MiB per connection)
+  if (c->fifo_slots == 0) c->fifo_slots = 2 * MCCS_BUFFER_SLOTS;
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
@@ -59,6 +64,7 @@ static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
   if (c.locality != MCCS_LOCALITY_SENDER && c.locality != MCCS_LOCALITY_RECEIVER) return mccsInvalidArgument;
   if (c.fifo_memory != MCCS_FIFO_UNCACHED && c.fifo_memory != MCCS_FIFO_DEVICE) return mccsInvalidArgument;
   if (nranks < 1 || nranks > 64) return mccsInvalidArgument;
+  if (c.fifo_slots != 8 && c.fifo_slots != 16 && c.fifo_slots != 32) return mccsInvalidArgument;
   return mccsSuccess;
 }
 
@@ -174,7 +180,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   cfg->bridge_streams = -1;
   // operator overrides (no rebuild needed): MCCS_LOCALITY=sender|receiver,
   // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE,
-  // MCCS_BRIDGE_STREAMS, MCCS_FIFO_MEMORY=uncached|device
+  // MCCS_BRIDGE_STREAMS, MCCS_FIFO_MEMORY=uncached|device, MCCS_FIFO_SLOTS
   if (const char* v = std::getenv("MCCS_LOCALITY"))
     cfg->locality = (v[0] == 's' || v[0] == 'S') ? MCCS_LOCALITY_SENDER : MCCS_LOCALITY_RECEIVER;
   if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
@@ -184,6 +190,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   if (const char* v = std::getenv("MCCS_BLOCK_THREADS")) cfg->block_threads = std::atoi(v);
   if (const char* v = std::getenv("MCCS_CHANNELS")) cfg->channel_count = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BUFFER_SIZE")) cfg->buffer_size = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_FIFO_SLOTS")) cfg->fifo_slots = std::atoi(v);
 }
 
 extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {

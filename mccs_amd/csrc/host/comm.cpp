@@ -95,6 +95,7 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
   mccsRingKernelCfg k{};
   k.fence_mode = c->all_uncached ? MCCS_FENCE_UNCACHED : MCCS_FENCE_SYSTEM;
   k.err_line = 1;  // d_abort is a 64-byte line of ours: errors go to its word 1
+  k.fifo_slots = (uint32_t)c->cfg.fifo_slots;
   const int tmo = c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms;
   k.timeout_ticks = tmo < 0 ? 0 : (uint64_t)tmo * 100000ull;  // s_memrealtime: 100 MHz
   // one 4-step slice per chunk (2 slices in flight per lane): one flag
@@ -160,6 +161,7 @@ mccsResult_t comm_alloc_local(Comm* c) {
   DeviceGuard g(c->device);
   c->layout.nch = c->nch;
   c->layout.buffer_size = (size_t)c->cfg.buffer_size;
+  c->layout.fifo_bytes = (size_t)c->cfg.buffer_size / MCCS_BUFFER_SLOTS * (size_t)c->cfg.fifo_slots;
   const size_t bytes = c->layout.total();
   c->own_arena = nullptr;
   c->own_arena_uncached = false;

@@ -58,16 +58,18 @@ struct DeviceGuard {
 };
 
 // Per-rank FIFO arena layout (identical on every rank; offsets in bytes).
-// [flags: nch x {send head lines, recv tail lines}] [data: nch x buffer_size]
+// [flags: nch x {send head lines, recv tail lines}] [data: nch x fifo_bytes]
+// fifo_bytes = fifo_slots x buffer_size / 8 (slots of the reference step size)
 struct ArenaLayout {
   int nch = 0;
   size_t buffer_size = 0;
+  size_t fifo_bytes = 0;
   static constexpr size_t kLinesBytes = (size_t)MCCS_MAX_LANES * MCCS_FLAG_LINE_BYTES;  // 8 KiB
   size_t head_off(int c) const { return (size_t)c * 2 * kLinesBytes; }
   size_t tail_off(int c) const { return (size_t)c * 2 * kLinesBytes + kLinesBytes; }
   size_t flags_bytes() const { return (((size_t)nch * 2 * kLinesBytes) + 65535) & ~(size_t)65535; }
-  size_t data_off(int c) const { return flags_bytes() + (size_t)c * buffer_size; }
-  size_t total() const { return flags_bytes() + (size_t)nch * buffer_size; }
+  size_t data_off(int c) const { return flags_bytes() + (size_t)c * fifo_bytes; }
+  size_t total() const { return flags_bytes() + (size_t)nch * fifo_bytes; }
 };
 
 // Connect handle exchanged between processes (fixed size, POD).

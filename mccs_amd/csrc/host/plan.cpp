@@ -331,7 +331,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     for (size_t k = 0; k < idx.size(); ++k) {
       const Comm* ck = comms[idx[k]];
       if (lds[k].mask != lds[0].mask || lds[k].multi_fn != lds[0].multi_fn || ck->lanes != c0->lanes ||
-          ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps)
+          ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps ||
+          ck->kcfg.fifo_slots != c0->kcfg.fifo_slots)
         return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
       ma.comm[k] = (mccsDevComm*)ck->d_comm;
       ma.work[k] = lds[k].work;

@@ -43,6 +43,9 @@ struct mccsRingKernelCfg {
                           // ours); 0: reference-named kernels, whose abortFlag is the caller's
                           // 4-byte allocation: only abortFlag itself is raised (the reference's
                           // one error channel, devcomm.h abortFlag)
+  uint32_t fifo_slots;    // physical FIFO slots (power of two >= MCCS_BUFFER_SLOTS): slot = step % fifo_slots,
+                          // a sender may run fifo_slots steps ahead; the reference has 8
+  uint32_t pad;
 };
 
 // Per-device ring profile counters (s_memrealtime ticks, 100 MHz), summed

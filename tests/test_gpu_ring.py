@@ -186,6 +186,10 @@ CONFIGS = [
     # not rotations of each other (ring.index relative to rank 0, userRanks)
     dict(channel_count=2, rings=[[3, 0, 6, 1, 7, 2, 5, 4], [4, 5, 2, 7, 1, 6, 0, 3]]),
     dict(channel_count=3, rings=[[5, 2, 0, 7, 4, 1, 6, 3]] * 3, lanes=2),
+    # deeper FIFOs (more slices in flight per lane; same chunk schedule)
+    dict(fifo_slots=16),
+    dict(fifo_slots=32, lanes=3, buffer_size=1 << 20),
+    dict(fifo_slots=16, locality=C.LOCALITY_SENDER, fifo_memory=C.FIFO_DEVICE),
 ]
 
 

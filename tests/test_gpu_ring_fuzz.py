@@ -1,7 +1,7 @@
 """GPU: seeded random ring configurations against the oracle.
 
 Each case draws the rank count, dtype, op, element count (ragged, sometimes
-tiny, sometimes several FIFO loops), channels, lanes, block size, FIFO
+tiny, sometimes several FIFO loops), channels, lanes, block size, FIFO depth, FIFO
 memory kind, data placement, slicing and an optional ring override, runs one
 grouped AllReduce (or AllGather) on a virtual node and compares every rank
 bit for bit with the oracle's restatement of the reference schedule.
@@ -44,6 +44,8 @@ def _case(seed):
         cfg["rings"] = [list(rng.permutation(n)) for _ in range(nch)]
     slice2 = bool(rng.random() < 0.25)
     gather = bool(rng.random() < 0.2)
+    if rng.random() < 0.3:
+        cfg["fifo_slots"] = int(rng.choice([16, 32]))
     return n, code, op, count, cfg, slice2, gather, rng
 
 

@@ -69,7 +69,8 @@ def test_requested_channel_count():
 def test_config_struct_matches_header():
     from mccs_amd._lib import _CommConfig
 
-    assert ctypes.sizeof(_CommConfig) == 9 * 4 + 4 + 8  # 9 ints, pad, pointer
+    assert ctypes.sizeof(_CommConfig) == 9 * 4 + 4 + 8 + 4 + 4  # 9 ints, pad, pointer, fifo_slots, pad
+    assert _CommConfig.fifo_slots.offset == 48
     lib = comm._sig()
     c = _CommConfig()
     lib.mccsCommConfigDefault(ctypes.byref(c))
