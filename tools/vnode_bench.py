@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--bridge", type=int, default=0, help="CommConfig.bridge_streams (0 = library default)")
     ap.add_argument("--profile", action="store_true", help="per-slice wait/stream timing (MCCS_RING_PROFILE)")
     ap.add_argument("--graph", action="store_true", help="also time the same calls captured in one HIP graph")
+    ap.add_argument("--allgather", action="store_true", help="time AllGather (size = bytes per rank) instead")
     args = ap.parse_args()
     if args.profile:
         os.environ["MCCS_RING_PROFILE"] = "1"
@@ -39,12 +40,18 @@ def main():
             for kib in (args.sizes_kib or [m << 10 for m in args.sizes_mib]):
                 cnt = (kib << 10) // 4
                 xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
-                ys = [torch.empty_like(x) for x in xs]
+                ys = [torch.empty(n * cnt if args.allgather else cnt, device="cuda") for _ in xs]
+
+                def call(r, st=None):
+                    if args.allgather:
+                        C.all_gather(comms[r], xs[r], ys[r], cnt * 4, stream=st)
+                    else:
+                        C.all_reduce(comms[r], xs[r], ys[r], cnt, C.AllReduceDataType.Float32, stream=st)
 
                 def once():
                     with C.group():
                         for r in range(n):
-                            C.all_reduce(comms[r], xs[r], ys[r], cnt, C.AllReduceDataType.Float32)
+                            call(r)
 
                 once()
                 for c in comms:
@@ -69,7 +76,7 @@ def main():
                         for _ in range(args.iters):
                             with C.group():
                                 for r in range(n):
-                                    C.all_reduce(comms[r], xs[r], ys[r], cnt, C.AllReduceDataType.Float32, stream=st)
+                                    call(r, st)
                     g.replay()
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
@@ -77,7 +84,7 @@ def main():
                     torch.cuda.synchronize()
                     graph_ms = (time.perf_counter() - t0) / args.iters * 1e3
                     del g
-                print(json.dumps({"n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels,
+                print(json.dumps({"coll": "allgather" if args.allgather else "allreduce", "n": n, "lanes": comms[0].lanes, "channels": comms[0].nchannels,
                                   "block": comms[0].block_threads, "bridge": args.bridge, "KiB": kib, "ms": round(dt * 1e3, 4),
                                   "algbw_GBps": round((kib << 10) / dt / 1e9, 2), "slice_profile": prof,
                                   "graph_ms": round(graph_ms, 4) if graph_ms else None,
