@@ -51,6 +51,37 @@ def test_allreduce_proto_kat(n):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_allgather_proto_kat(n):
+    """allgather_proto (src/mccs_examples/allgather_proto/src/main.rs:27-115):
+    one buffer of n x size bytes per rank, rank r fills its own segment with
+    int32 2042 + r and AllGathers IN PLACE (send = buffer + r x size); every
+    rank must then hold 2042 + r in segment r (the reference checks the first
+    word of each segment; here every word).  size = 1 MiB, as the example's
+    --size 1."""
+    import torch
+
+    comms = C.init_all([0] * n)
+    try:
+        size = 1 << 20
+        words = size // 4
+        bufs = []
+        for r in range(n):
+            b = torch.zeros(n * words, dtype=torch.int32, device="cuda")
+            b[r * words:(r + 1) * words] = 2042 + r
+            bufs.append(b)
+        with C.group():
+            for r in range(n):
+                C.all_gather(comms[r], bufs[r][r * words:], bufs[r], size)
+        for c in comms:
+            c.sync()
+        want = torch.arange(n, dtype=torch.int32, device="cuda").repeat_interleave(words) + 2042
+        for r in range(n):
+            assert torch.equal(bufs[r], want), r
+    finally:
+        vnode.destroy(comms)
+
+
 @pytest.mark.parametrize("n", [4, 8])
 @pytest.mark.parametrize("code", [F16, F32])
 def test_exact_sum_inputs(n, code):

@@ -1,9 +1,10 @@
 """CPU tests: pin the C oracle (oracle/mccs_oracle.c) before trusting it.
 
 Pins, in order of strength:
-  * reference known-answer test allreduce_proto (src/mccs_examples/
+  * reference known-answer tests allreduce_proto (src/mccs_examples/
     allreduce_proto/src/main.rs:27,75-116): int32 Sum, rank r holds 2042+r,
-    every element == 2042*n + n(n-1)/2;
+    every element == 2042*n + n(n-1)/2; and allgather_proto
+    (allgather_proto/src/main.rs:27-115): segment r == 2042 + r;
   * exact-sum fp inputs (values k/64, |k| <= 255) whose sum is exact in any
     order, checked against the float64 sum (nccl-tests verifiable design,
     nccl-tests-mccs/verifiable/verifiable.cu:419-520);
@@ -143,6 +144,17 @@ def test_allreduce_proto_kat(orc, n):
     inputs = [np.full(count, 2042 + r, dtype=np.int32) for r in range(n)]
     out = orc.ring_allreduce(I32, 0, inputs, nchannels=2, nthreads=544)
     assert np.all(out == 2042 * n + n * (n - 1) // 2)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_allgather_proto_kat(orc, n):
+    # allgather_proto (src/mccs_examples/allgather_proto/src/main.rs:27-115):
+    # rank r contributes a segment of int32 2042 + r; after the AllGather
+    # segment r holds 2042 + r on every rank (1 MiB segments, --size 1)
+    words = (1 << 20) // 4
+    inputs = [np.full(words, 2042 + r, dtype=np.int32) for r in range(n)]
+    out = orc.ring_allgather(inputs).view(np.int32)
+    assert np.array_equal(out, np.repeat(np.arange(n, dtype=np.int32) + 2042, words))
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
