@@ -117,8 +117,8 @@ __device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1,
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (q + 64u * u < npack)
-          v[u] = (u < PF && use_pre) ? pre[u < PF ? u : 0]
-                                     : ld16<(NTMASK & 1) ? kNonTemporal : kPlain>(a + q + 64u * u);
+          v[u] = (u < PF && use_pre && base == 0) ? pre[u < PF ? u : 0]
+                                                  : ld16<(NTMASK & 1) ? kNonTemporal : kPlain>(a + q + 64u * u);
       if constexpr (NS > 1) {
         u32x4 w[U];
 #pragma unroll
