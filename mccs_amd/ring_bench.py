@@ -173,12 +173,15 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
              ranks_share_gpu=False, rejected=None):
     """Transport placement chosen on the node itself: FIFO data at the
     receiver (remote writes) or at the sender (remote reads, the reference's
-    SHM layout), each at the auto lane count and at 16 lanes per channel.
+    SHM layout), each at the auto lane count and at 16 and 32 lanes per
+    channel (a lane count equal to auto is timed once).
     Every candidate passes the exact-sum gate; the fastest (max over ranks)
     is kept.  MCCS_LOCALITY / MCCS_LANES pin a dimension.
     Returns (comm, mode, table)."""
     locs = [None] if "MCCS_LOCALITY" in os.environ else [C.LOCALITY_RECEIVER, C.LOCALITY_SENDER]
-    lanes_opts = [None] if "MCCS_LANES" in os.environ else [None, 16]
+    # lanes per channel: auto (64 / channels; 9 at n = 8), 16 and 32 -- more
+    # lanes keep more bytes in flight per xGMI link, at more flag traffic
+    lanes_opts = [None] if "MCCS_LANES" in os.environ else [None, 16, 32]
     if ranks_share_gpu and "MCCS_LANES" not in os.environ:
         lanes_opts = [shared_gpu_lanes(world)]
     best, table, seen = None, [], set()
