@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -192,6 +193,45 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld) {
   return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
 }
 
+// A launch whose ranks' used channels each hold one work carries the works in
+// its arguments (mccsMultiLaunchArgs.inline_work, ring_cfg.h): no FIFO slot,
+// no acknowledgement, and no PCIe read in the kernel prologue.  Returns the
+// channels used per rank (0: use the work FIFO).  MCCS_INLINE_WORKS=0 turns it
+// off.
+static int inline_channels(const Comm* c) {
+  static const bool enabled = [] {
+    const char* v = std::getenv("MCCS_INLINE_WORKS");
+    return !(v && std::atoi(v) == 0);
+  }();
+  if (!enabled) return 0;
+  int used = 0;
+  for (int ch = 0; ch < c->nch; ++ch) {
+    const size_t w = c->sched[ch].works.size();
+    if (w > 1) return 0;
+    used += w == 1;
+  }
+  return used;
+}
+
+static mccsResult_t upload_work_inline(Comm* c, LaunchDesc* ld, mccsMultiLaunchArgs* ma) {
+  uint64_t mask = 0;
+  uint32_t n = 0;
+  for (int ch = 0; ch < c->nch; ++ch)
+    if (!c->sched[ch].works.empty()) {
+      mask |= 1ull << ch;
+      ma->inline_work[ma->inline_works + n++] = to_dev_work(c->sched[ch].works[0], false, true, 0);
+    }
+  ma->inline_works += n;
+  ld->mask = mask;
+  ld->nch_used = (int)n;
+  ld->work = nullptr;
+  ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
+  ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
+  for (auto& s : c->sched) s = ChannelSchedule{};
+  c->plan_pending = false;
+  return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
+}
+
 static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
   std::vector<int> chan_list;
   uint64_t mask = 0;
@@ -302,8 +342,17 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     bool capturing = false;
     MCCS_HIP(rt().StreamIsCapturing(user_streams[idx[0]], &capturing));
     std::vector<LaunchDesc> lds(idx.size());
-    for (size_t k = 0; k < idx.size(); ++k)
-      MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k]) : upload_work(comms[idx[k]], &lds[k]));
+    mccsMultiLaunchArgs ma;
+    std::memset(&ma, 0, sizeof(ma));
+    int per_rank = inline_channels(comms[idx[0]]);
+    for (size_t k = 1; k < idx.size() && per_rank > 0; ++k)
+      if (inline_channels(comms[idx[k]]) != per_rank) per_rank = 0;
+    if (per_rank > 0 && per_rank * idx.size() <= MCCS_INLINE_WORKS) {
+      for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work_inline(comms[idx[k]], &lds[k], &ma));
+    } else {
+      for (size_t k = 0; k < idx.size(); ++k)
+        MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k]) : upload_work(comms[idx[k]], &lds[k]));
+    }
     Comm* c0 = comms[idx[0]];
     const bool bridge = c0->cfg.bridge_streams >= 0;
     hipStream_t st = user_streams[idx[0]];
@@ -324,8 +373,6 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     // (one launch per device; blockIdx.y = rank slot when ranks share it).
     // Fused ranks take the safest policy of the group.
     if (idx.size() > MCCS_MULTI_MAX_RANKS) return mccsInvalidUsage;
-    mccsMultiLaunchArgs ma;
-    std::memset(&ma, 0, sizeof(ma));
     ma.channelMask = lds[0].mask;
     ma.cfg = c0->kcfg;
     for (size_t k = 0; k < idx.size(); ++k) {

@@ -11,6 +11,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "mccs_devcomm.h"
+
 #define MCCS_FLAG_LINE_BYTES 128
 #define MCCS_FLAG_LINE_WORDS (MCCS_FLAG_LINE_BYTES / 8)
 #define MCCS_MAX_LANES 64
@@ -60,9 +62,22 @@ struct mccsRingKernelCfg {
 // launch (several when ranks share a GPU: tests' virtual node).
 // blockIdx.y = rank slot.
 #define MCCS_MULTI_MAX_RANKS 16
+// A launch whose ranks' channels each run one work may carry those works in
+// its arguments (kernarg memory is device memory on MI355X) instead of the
+// host-mapped work FIFO, whose read over PCIe is the long pole of the kernel
+// prologue; inFifo = 0, so nothing is acknowledged.  Rank slot k's works are
+// inline_work[k * channels used ...].  7 works = the n = 8 rings and keeps the
+// arguments under 4 KiB.
+#define MCCS_INLINE_WORKS 7
 struct mccsMultiLaunchArgs {
   struct mccsDevComm* comm[MCCS_MULTI_MAX_RANKS];
   struct mccsDevWork* work[MCCS_MULTI_MAX_RANKS];
   uint64_t channelMask;
   struct mccsRingKernelCfg cfg;  // this launch's hand-off policy
+  uint32_t inline_works;         // > 0: the works are inline_work[0 .. inline_works)
+  uint32_t pad3[3];
+  struct mccsDevWork inline_work[MCCS_INLINE_WORKS];
 };
+#ifdef __cplusplus
+static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must stay within 4 KiB");
+#endif
