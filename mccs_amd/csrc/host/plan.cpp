@@ -199,11 +199,8 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld) {
 // channels used per rank (0: use the work FIFO).  MCCS_INLINE_WORKS=0 turns it
 // off.
 static int inline_channels(const Comm* c) {
-  static const bool enabled = [] {
-    const char* v = std::getenv("MCCS_INLINE_WORKS");
-    return !(v && std::atoi(v) == 0);
-  }();
-  if (!enabled) return 0;
+  const char* v = std::getenv("MCCS_INLINE_WORKS");  // read per launch: tests switch it
+  if (v && std::atoi(v) == 0) return 0;
   int used = 0;
   for (int ch = 0; ch < c->nch; ++ch) {
     const size_t w = c->sched[ch].works.size();

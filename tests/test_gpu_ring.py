@@ -440,14 +440,19 @@ def test_ring_profile_counters(monkeypatch):
         C.init_all([0])[0].destroy()  # disarm
 
 
-@pytest.mark.parametrize("n,count,bridge", [(2, 1 << 20, None), (4, 300007, None), (2, 77777, 1)])
-def test_allreduce_captured_in_hip_graph(orc, n, count, bridge):
+@pytest.mark.parametrize("n,count,bridge,fifo", [(2, 1 << 20, None, False), (2, 1 << 20, None, True),
+                                                 (4, 300007, None, False), (2, 77777, 1, False)])
+def test_allreduce_captured_in_hip_graph(orc, n, count, bridge, fifo, monkeypatch):
     """AllReduces captured into a HIP graph (torch.cuda.graph) replay with the
     inputs of each replay, interleaved with eager calls on the same comms:
-    captured work lists live outside the rolling work FIFO, and the FIFO
-    steps persisted in device memory keep eager and replayed launches in
+    captured work lists live outside the rolling work FIFO (in the launch
+    arguments, or -- fifo=True -- in the graph arena), and the FIFO steps
+    persisted in device memory keep eager and replayed launches in
     lock-step."""
     import torch
+
+    if fifo:
+        monkeypatch.setenv("MCCS_INLINE_WORKS", "0")
 
     # bridge=1: launches go to the comm's own stream, joined to the capturing
     # stream by events (libmccs two-stream bridge)
@@ -535,13 +540,15 @@ def test_allreduce_zero_count_is_noop():
 
 
 @pytest.mark.parametrize("depth", [8, 16])
-def test_work_fifo_wraps_and_flow_controls(orc, depth):
+def test_work_fifo_wraps_and_flow_controls(orc, depth, monkeypatch):
     """A tiny work FIFO (plan.rs:380-541: rolling work_queue indices, restart
     at slot 0 on wrap, wait_work_queue on workFifoDone acks) over many calls:
     every call's work list wraps the ring several times and the host must
-    wait for the kernel's acks before reusing slots."""
+    wait for the kernel's acks before reusing slots.  (Works that fit the
+    launch arguments skip the FIFO: forced off here.)"""
     import torch
 
+    monkeypatch.setenv("MCCS_INLINE_WORKS", "0")
     n = 2
     comms = C.init_all([0] * n, C.CommConfig(work_fifo_depth=depth))
     try:

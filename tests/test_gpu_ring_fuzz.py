@@ -46,14 +46,17 @@ def _case(seed):
     gather = bool(rng.random() < 0.2)
     if rng.random() < 0.3:
         cfg["fifo_slots"] = int(rng.choice([16, 32]))
-    return n, code, op, count, cfg, slice2, gather, rng
+    fifo_works = bool(rng.random() < 0.3)  # work list through the FIFO even where it fits the launch arguments
+    return n, code, op, count, cfg, slice2, gather, fifo_works, rng
 
 
 @pytest.mark.parametrize("seed", range(CASES))
 def test_random_ring_case(orc, seed, monkeypatch):
-    n, code, op, count, cfg, slice2, gather, rng = _case(1000 + seed)
+    n, code, op, count, cfg, slice2, gather, fifo_works, rng = _case(1000 + seed)
     if slice2:
         monkeypatch.setenv("MCCS_SLICE_STEPS", "2")
+    if fifo_works:
+        monkeypatch.setenv("MCCS_INLINE_WORKS", "0")
     comms = C.init_all([0] * n, C.CommConfig(**cfg))
     try:
         if gather:
