@@ -202,12 +202,15 @@ class FakeRuntime final : public DeviceRuntime {
   hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
     // every communicator of a fused ring launch must live on the launching device
     bool on_dev = true;
+    unsigned inl = 0;
     if (fn && args && grid.y >= 1 && grid.y <= MCCS_MULTI_MAX_RANKS) {
       const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
       for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(ma->comm[k]) == cur_;
+      inl = ma->inline_works;
     }
     note("launch dev=" + std::to_string(cur_) + " grid=" + std::to_string(grid.x) + "x" + std::to_string(grid.y) +
-         " block=" + std::to_string(block.x) + " stream=" + sid(s) + " comms_on_dev=" + (on_dev ? "1" : "0"));
+         " block=" + std::to_string(block.x) + " stream=" + sid(s) + " comms_on_dev=" + (on_dev ? "1" : "0") +
+         " inline_works=" + std::to_string(inl));
     return hipSuccess;
   }
   hipError_t BlocksPerCu(int* per_cu, const void*, int) override {

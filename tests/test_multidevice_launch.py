@@ -84,6 +84,8 @@ def test_init_all_eight_devices_one_launch_per_device(fake):
         ev = _log()
         launches = _check_launch_phase(ev, 8, 1, nch * lanes)
         assert len(launches) == 8
+        # one work per ring: the 7 works travel in the launch arguments
+        assert all(kv["inline_works"] == "7" for _, kv in launches), launches
         for c in comms:
             c.sync()
         ev = _log()
@@ -109,6 +111,32 @@ def test_back_to_back_groups_issue_without_host_waits(fake):
             c.destroy()
 
 
+def test_work_list_falls_back_to_the_fifo(fake, monkeypatch):
+    """Works go through the reference's work FIFO when they do not fit the
+    launch arguments: several collectives of a group on one channel (chained
+    works), or MCCS_INLINE_WORKS=0."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
+    try:
+        _log()
+        with C.group():
+            # 12 grouped 4 MiB AllReduces, each on all 7 channels: 12 elements per
+            # channel = 2 chained works (MCCS_MAX_WORK_ELEMENTS = 10 per work)
+            for _ in range(12):
+                for r, c in enumerate(comms):
+                    C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 1 << 20, F32, SUM,
+                                 stream=0)
+        launches = [kv for k, kv in _log() if k == "launch"]
+        assert len(launches) == 8 and all(kv["inline_works"] == "0" for kv in launches), launches
+        monkeypatch.setenv("MCCS_INLINE_WORKS", "0")
+        _allreduce_group(comms)
+        launches = [kv for k, kv in _log() if k == "launch"]
+        assert len(launches) == 8 and all(kv["inline_works"] == "0" for kv in launches), launches
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_colocated_ranks_are_fused_per_device(fake):
     """Two ranks per device (4 devices): one launch per device, blockIdx.y = rank slot."""
     fake(4)
@@ -120,6 +148,8 @@ def test_colocated_ranks_are_fused_per_device(fake):
         ev = _log()
         launches = _check_launch_phase(ev, 4, 2, comms[0].nchannels * 2)
         assert len(launches) == 4
+        # 2 ranks x 7 channels = 14 works > MCCS_INLINE_WORKS (7): the work FIFO
+        assert all(kv["inline_works"] == "0" for _, kv in launches), launches
     finally:
         for c in comms:
             c.destroy()
