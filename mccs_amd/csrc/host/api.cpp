@@ -101,12 +101,14 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   c->cfg.rings = nullptr;  // not owned
   c->nch = (int)c->rings.size();
   c->block_threads = cfg.block_threads;
-  // auto lanes: ~64 streaming workgroups per rank.  A lane's throughput is
-  // bound by its per-slice latency chain (flag poll, loads, store drain), not
-  // by bandwidth: the 2-rank virtual node at 128 MiB runs 335 / 488 / 499
-  // GB/s at 16 / 32 / 64 lanes per channel; an 8-GPU rank must feed 7 links x
+  // auto lanes: ~64 streaming workgroups per rank (128 at n = 2).  A lane's
+  // throughput is bound by its per-slice latency chain (flag poll, loads,
+  // store drain), not by bandwidth: the 2-rank virtual node at 128 MiB runs
+  // 335 / 488 / 499 GB/s at 2 channels x 16 / 32 / 64 lanes and 754 at
+  // 4 x 32 (comm.cpp default_rings); an 8-GPU rank must feed 7 links x
   // ~77 GB/s per direction (7 channels x 9 lanes).
-  c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, 64 / c->nch)));
+  const int wgs = nranks == 2 ? 128 : 64;
+  c->lanes = cfg.lanes > 0 ? cfg.lanes : (nranks == 1 ? 1 : std::max(1, std::min(MCCS_MAX_LANES, wgs / c->nch)));
   // every lane owns a >= 256-byte region of each 2-step slot pair (ring.hip)
   while (c->lanes > 1 && (size_t)cfg.buffer_size / MCCS_BUFFER_SLOTS * 2 / c->lanes < 256) {
     if (cfg.lanes > 0) {

@@ -85,7 +85,12 @@ void default_rings(int n, int nch_req, std::vector<std::vector<int>>* rings) {
       base.push_back(r);
     }
   }
-  int nch = nch_req > 0 ? nch_req : (n <= 2 ? 2 : (int)base.size());
+  // n = 2: one ring, 4 channels of it.  A channel keeps one 4-step slice per
+  // lane in flight, so the bytes a rank has in flight grow with channels x
+  // slice, not with lanes (2-rank virtual node, 128 MiB, graph replay: 2 x 32
+  // lanes 507 GB/s, 4 x 16 541, 4 x 32 754, 8 x 16 751).  Two-term sums
+  // commute, so the channel count leaves every n = 2 result unchanged.
+  int nch = nch_req > 0 ? nch_req : (n == 2 ? 4 : n == 1 ? 2 : (int)base.size());
   nch = std::min(nch, (int)MCCS_MAX_NCHANNELS);
   for (int c = 0; c < nch; ++c) rings->push_back(base[c % base.size()]);
 }

@@ -214,8 +214,8 @@ def shared_gpu_lanes(world: int) -> int:
     rehearsal): separate processes' ring kernels must all be resident at once
     and the GPU does not guarantee that for many large grids (4 processes x
     60 workgroups timed out on MI355X; 4 lanes ran), so keep them small;
-    two processes x 2 channels x 32 lanes = 128 workgroups fit."""
-    return 32 if world <= 2 else 4
+    two processes x 4 channels x 16 lanes = 128 workgroups fit."""
+    return 16 if world <= 2 else 4
 
 
 def graph_replay(torch, dist, comm, call_on, calls=10):

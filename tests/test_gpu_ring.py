@@ -245,10 +245,11 @@ def test_configs(orc, cfg):
 @pytest.mark.parametrize("count", [5000, 777777, (37 << 20) // 4 + 3])
 def test_wide_lanes(orc, lanes, count):
     """Up to MCCS_MAX_LANES = 64 workgroups per channel (a 2-rank virtual node
-    then fills every CU): each lane owns a fixed 256-byte-aligned region of a
-    slot group, 32 KiB at 64 lanes; bit-exact, multi-loop sizes included."""
+    of 2 channels then fills every CU): each lane owns a fixed 256-byte-aligned
+    region of a slot group, 32 KiB at 64 lanes; bit-exact, multi-loop sizes
+    included."""
     n = 2
-    comms = C.init_all([0] * n, C.CommConfig(lanes=lanes))
+    comms = C.init_all([0] * n, C.CommConfig(lanes=lanes, channel_count=2))
     try:
         rng = np.random.default_rng(lanes + count)
         inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
