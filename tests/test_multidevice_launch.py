@@ -111,6 +111,20 @@ def test_back_to_back_groups_issue_without_host_waits(fake):
             c.destroy()
 
 
+@pytest.mark.parametrize("n,nch,lanes", [(2, 4, 32), (4, 6, 10), (8, 7, 9)])
+def test_default_channels_and_lanes(fake, n, nch, lanes):
+    """One rank per device: n = 2 runs 4 channels of its ring x 32 lanes
+    (128 workgroups), n = 4 its 6 directed rings x 10, n = 8 its 7
+    arc-disjoint rings x 9 (lanes)."""
+    fake(n)
+    comms = C.init_all(list(range(n)), C.CommConfig())
+    try:
+        assert [(c.nchannels, c.lanes) for c in comms] == [(nch, lanes)] * n
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_work_list_falls_back_to_the_fifo(fake, monkeypatch):
     """Works go through the reference's work FIFO when they do not fit the
     launch arguments: several collectives of a group on one channel (chained
