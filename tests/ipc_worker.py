@@ -48,10 +48,14 @@ def main():
                  "sender-device": (C.FIFO_DEVICE, C.LOCALITY_SENDER)}
     names = os.environ.get("IPC_MODES", "uncached,device").split(",")
     results = {}
+    # two processes on one GPU: their kernels must be co-resident, so keep the
+    # pair at 128 workgroups (4 channels x 16 lanes, ring_bench.shared_gpu_lanes)
+    # rather than the node default of 128 per rank
+    lanes = 16 if world == 2 and torch.cuda.device_count() < world else None
     for mode in names:
         fifo, loc = all_modes[mode]
         comm = C.init_communicator_rank(rank, world, dev, exchange,
-                                        C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000))
+                                        C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, lanes=lanes))
         cases = [(2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)]
         nfuzz = int(os.environ.get("IPC_FUZZ", "0"))
         if nfuzz:  # seeded random dtypes / ragged counts, same on every rank
