@@ -206,7 +206,9 @@ mccsResult_t comm_alloc_local(Comm* c) {
 
   MCCS_HIP(rt().Malloc((void**)&c->d_abort, 64));
   MCCS_HIP(rt().Memset(c->d_abort, 0, 64));  // the reference leaves it uninitialised (device.rs:157)
-  MCCS_HIP(rt().Malloc((void**)&c->d_comm, sizeof(mccsDevCommAndChannels)));
+  MCCS_HIP(rt().Malloc((void**)&c->d_comm,
+                       sizeof(mccsDevCommAndChannels) + sizeof(mccsRingConnView) * MCCS_MAX_NCHANNELS));
+  c->d_view = (mccsRingConnView*)((char*)c->d_comm + sizeof(mccsDevCommAndChannels));
   c->d_peers.assign(c->nch, nullptr);
   c->d_user_ranks.assign(c->nch, nullptr);
   for (int ch = 0; ch < c->nch; ++ch) {
@@ -246,6 +248,8 @@ mccsResult_t comm_build_device(Comm* c) {
   hc.comm.nRanks = n;
   hc.comm.buffSizes[MCCS_PROTO_SIMPLE] = c->cfg.buffer_size;
   hc.comm.abortFlag = c->d_abort;
+  mccsRingConnView views[MCCS_MAX_NCHANNELS];
+  std::memset(views, 0, sizeof(views));
   for (int ch = 0; ch < c->nch; ++ch) {
     const std::vector<int>& ring = c->rings[ch];
     const int ix_rank = (int)(std::find(ring.begin(), ring.end(), c->rank) - ring.begin());
@@ -272,6 +276,7 @@ mccsResult_t comm_build_device(Comm* c) {
       r.buffs[MCCS_PROTO_SIMPLE] = sender_local ? pv + L.data_off(ch) : me + L.data_off(ch);
       r.tail = (uint64_t*)(me + L.tail_off(ch));
       r.head = (uint64_t*)(pv + L.head_off(ch));
+      views[ch] = {r.buffs[MCCS_PROTO_SIMPLE], s.buffs[MCCS_PROTO_SIMPLE], r.tail, r.head, s.head, s.tail};
     }
     MCCS_HIP(rt().Memcpy(c->d_peers[ch], peers.data(), sizeof(mccsDevChannelPeer) * n, hipMemcpyHostToDevice));
     MCCS_HIP(rt().Memcpy(c->d_user_ranks[ch], user_ranks.data(), sizeof(int) * n, hipMemcpyHostToDevice));
@@ -284,6 +289,7 @@ mccsResult_t comm_build_device(Comm* c) {
     dc.workFifoDone = c->d_done + ch;
   }
   MCCS_HIP(rt().Memcpy(c->d_comm, &hc, sizeof(hc), hipMemcpyHostToDevice));
+  MCCS_HIP(rt().Memcpy(c->d_view, views, sizeof(views), hipMemcpyHostToDevice));
   MCCS_CHECK(comm_set_kernel_cfg(c));
   c->connected = true;
   return mccsSuccess;

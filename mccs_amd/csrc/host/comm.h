@@ -117,6 +117,7 @@ struct Comm {
   mccsDevCommAndChannels* d_comm = nullptr;
   std::vector<mccsDevChannelPeer*> d_peers;
   std::vector<int*> d_user_ranks;
+  mccsRingConnView* d_view = nullptr;  // per channel, in d_comm's allocation after the channels
   uint32_t* d_abort = nullptr;
   // host-mapped work FIFO (comm/mod.rs MCCS_WORK_FIFO_DEPTH) + done counters
   mccsDevWork* h_work = nullptr;

@@ -380,6 +380,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
         return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
       ma.comm[k] = (mccsDevComm*)ck->d_comm;
       ma.work[k] = lds[k].work;
+      ma.view[k] = ck->d_view;
       if (ck->kcfg.fence_mode != MCCS_FENCE_UNCACHED) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
       ma.cfg.timeout_ticks = (ma.cfg.timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)
                                  ? 0

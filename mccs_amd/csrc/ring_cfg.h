@@ -69,9 +69,23 @@ struct mccsRingKernelCfg {
 // inline_work[k * channels used ...].  7 works = the n = 8 rings and keeps the
 // arguments under 4 KiB.
 #define MCCS_INLINE_WORKS 7
+// The connector addresses one channel's lanes need (the prev recv and next
+// send mccsDevConnInfo fields), kept by this library beside its device
+// communicator (comm.cpp comm_build_device): a launch loads them together with
+// the communicator instead of one dependent round trip later through
+// mccsDevChannel.peers.  Reference-built communicators have none (view = 0).
+struct mccsRingConnView {
+  char* rbuf;        // receive FIFO data
+  char* sbuf;        // send FIFO data
+  uint64_t* r_tail;  // recv: polled (ours)
+  uint64_t* r_head;  // recv: posted (prev's)
+  uint64_t* s_head;  // send: polled (ours)
+  uint64_t* s_tail;  // send: posted (next's)
+};
 struct mccsMultiLaunchArgs {
   struct mccsDevComm* comm[MCCS_MULTI_MAX_RANKS];
   struct mccsDevWork* work[MCCS_MULTI_MAX_RANKS];
+  const struct mccsRingConnView* view[MCCS_MULTI_MAX_RANKS];  // per channel id; 0: use comm's peers
   uint64_t channelMask;
   struct mccsRingKernelCfg cfg;  // this launch's hand-off policy
   uint32_t inline_works;         // > 0: the works are inline_work[0 .. inline_works)
