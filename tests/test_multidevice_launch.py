@@ -125,6 +125,35 @@ def test_default_channels_and_lanes(fake, n, nch, lanes):
             c.destroy()
 
 
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_connector_views_match_the_peers(fake, n):
+    """The per-channel connector views communicator launches load
+    (ring_cfg.h mccsRingConnView, right after mccsDevCommAndChannels in the
+    device communicator's allocation) hold exactly the prev-recv / next-send
+    mccsDevConnInfo addresses the reference-named kernels read through
+    mccsDevChannel.peers (the fake runtime keeps device memory in host RAM)."""
+    from mccs_amd import abi
+
+    fake(n)
+    comms = C.init_all(list(range(n)), C.CommConfig())
+    try:
+        for c in comms:
+            base = c.dev_comm()
+            dc = abi.mccsDevCommAndChannels.from_address(base)
+            views = (ctypes.c_void_p * (6 * abi.MCCS_MAX_NCHANNELS)).from_address(
+                base + ctypes.sizeof(abi.mccsDevCommAndChannels))
+            for ch in range(c.nchannels):
+                chan = dc.channels[ch]
+                peers = (abi.mccsDevChannelPeer * n).from_address(chan.peers)
+                r = peers[chan.ring.prev].recv[0]
+                s = peers[chan.ring.next].send[0]
+                want = [r.buffs[0], s.buffs[0], r.tail, r.head, s.head, s.tail]
+                assert list(views[6 * ch:6 * ch + 6]) == want and all(want), (c.rank, ch)
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_work_list_falls_back_to_the_fifo(fake, monkeypatch):
     """Works go through the reference's work FIFO when they do not fit the
     launch arguments: several collectives of a group on one channel (chained
