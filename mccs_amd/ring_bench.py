@@ -108,19 +108,42 @@ DTYPES = {"float32": ("f32", "Float32", "float"), "float16": ("f16", "Float16", 
           "bfloat16": ("bf16", "Bfloat16", "__nv_bfloat16")}
 
 
-def _candidates(C, lanes_opts, locs):
+# A rank's workgroups must all be resident at once: channels x lanes beyond
+# this is never a candidate (one 576-thread ring workgroup per CU).
+MAX_RING_WORKGROUPS = 256
+
+
+def _candidates(C, lanes_opts, locs, chan_opts=(None,)):
     """Transport candidates in preference order; within one (placement,
-    lanes) the cached-FIFO arena is used only if the uncached one cannot be
-    created or exported."""
+    channels, lanes) the cached-FIFO arena is used only if the uncached one
+    cannot be created or exported."""
     out = []
     for loc in locs:
         lname = {None: "env", C.LOCALITY_RECEIVER: "receiver", C.LOCALITY_SENDER: "sender"}[loc]
-        for lanes in lanes_opts:
-            out.append((f"{lname}/lanes={lanes or 'auto'}",
-                        [(f"{lname}-uncached-fifo", C.CommConfig(locality=loc, lanes=lanes, timeout_ms=60000)),
-                         (f"{lname}-cached-fifo+system-fences",
-                          C.CommConfig(locality=loc, lanes=lanes, fifo_memory=C.FIFO_DEVICE, timeout_ms=60000))]))
+        for nch in chan_opts:
+            for lanes in lanes_opts:
+                if nch and lanes and nch * lanes > MAX_RING_WORKGROUPS:
+                    continue
+                kw = dict(locality=loc, lanes=lanes, timeout_ms=60000)
+                if nch:
+                    kw["channel_count"] = nch
+                tag = f"{lname}/lanes={lanes or 'auto'}" + (f"/channels={nch}" if nch else "")
+                out.append((tag, [(f"{lname}-uncached-fifo", C.CommConfig(**kw)),
+                                  (f"{lname}-cached-fifo+system-fences",
+                                   C.CommConfig(fifo_memory=C.FIFO_DEVICE, **kw))]))
     return out
+
+
+def channel_options(C, world: int, ranks_share_gpu: bool) -> list:
+    """Channel counts the autotune times: the default (one channel per ring,
+    4 at n = 2) and, on distinct GPUs, twice that (every ring twice).  A lane
+    keeps one slice of its channel in flight, so a rank's bytes in flight grow
+    with channels, not lanes (lanes); two channels per ring put
+    two slices on each xGMI link at once.  Results stay the reference
+    algorithm's for the chosen channel count (exact-sum gated)."""
+    if ranks_share_gpu or world < 2 or "MCCS_CHANNELS" in os.environ:
+        return [None]
+    return [None, 2 * len(C.default_rings(world, 0))]
 
 
 def make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, modes, full, group=None,
@@ -174,9 +197,11 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
     """Transport placement chosen on the node itself: FIFO data at the
     receiver (remote writes) or at the sender (remote reads, the reference's
     SHM layout), each at the auto lane count and at 16 and 32 lanes per
-    channel (a lane count equal to auto is timed once).
+    channel (a lane count equal to auto is timed once), and on distinct GPUs
+    at the default and twice the default channel count (channel_options; at
+    most MAX_RING_WORKGROUPS workgroups per rank).
     Every candidate passes the exact-sum gate; the fastest (max over ranks)
-    is kept.  MCCS_LOCALITY / MCCS_LANES pin a dimension.
+    is kept.  MCCS_LOCALITY / MCCS_LANES / MCCS_CHANNELS pin a dimension.
     Returns (comm, mode, table)."""
     locs = [None] if "MCCS_LOCALITY" in os.environ else [C.LOCALITY_RECEIVER, C.LOCALITY_SENDER]
     # lanes per channel: auto (64 / channels; 9 at n = 8), 16 and 32 -- more
@@ -184,20 +209,22 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
     lanes_opts = [None] if "MCCS_LANES" in os.environ else [None, 16, 32]
     if ranks_share_gpu and "MCCS_LANES" not in os.environ:
         lanes_opts = [shared_gpu_lanes(world)]
+    chan_opts = channel_options(C, world, ranks_share_gpu)
     best, table, seen = None, [], set()
-    for label, modes in _candidates(C, lanes_opts, locs):
+    for label, modes in _candidates(C, lanes_opts, locs, chan_opts):
         comm, mode = make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, modes, full,
                                          rejected=rejected)
         if comm is None:
             table.append({"mode": label, "created": False})
             continue
-        key = (mode, comm.lanes)
+        key = (mode, comm.nchannels, comm.lanes)
         if key in seen:  # auto lanes already == 16
             comm.destroy()
             continue
         seen.add(key)
         el = max_over_ranks(dist, time_steps(torch, dist, comm, step_for(comm), warmup, reps))
-        table.append({"mode": mode, "lanes": comm.lanes, "ms_per_step": round(el / reps * 1e3, 4)})
+        table.append({"mode": mode, "channels": comm.nchannels, "lanes": comm.lanes,
+                      "ms_per_step": round(el / reps * 1e3, 4)})
         if best is None or el < best[0]:
             if best is not None:
                 best[1].destroy()

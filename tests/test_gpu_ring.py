@@ -37,10 +37,14 @@ def test_allreduce_matches_oracle(orc, n, code):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("doubled", [False, True])
 @pytest.mark.parametrize("n", [2, 4, 8])
-def test_allreduce_proto_kat(n):
-    """allreduce_proto: int32 Sum, rank r holds 2042+r (scaled to 2 ring loops + tail)."""
-    comms = C.init_all([0] * n)
+def test_allreduce_proto_kat(n, doubled):
+    """allreduce_proto: int32 Sum, rank r holds 2042+r (scaled to 2 ring loops
+    + tail); also with twice the default channels (every ring twice, as the
+    bench autotune tries on distinct GPUs)."""
+    nch = 2 * len(C.default_rings(n, 0)) if doubled else None
+    comms = C.init_all([0] * n, C.CommConfig(channel_count=nch))
     try:
         count = 2 * comms[0].nchannels * n * (1 << 20) // 4 + 999
         inputs = [np.full(count, 2042 + r, dtype=np.int32) for r in range(n)]
@@ -212,6 +216,7 @@ CONFIGS = [
     dict(buffer_size=1 << 20),
     dict(channel_count=2, rings="default", block_threads=544, lanes=1),  # reference profile
     dict(channel_count=5),
+    dict(channel_count=14),  # every ring twice (the bench autotune's doubled channels)
     dict(bridge_streams=1),
     # comm_patterns_override with rings that do not start at rank 0 and are
     # not rotations of each other (ring.index relative to rank 0, userRanks)

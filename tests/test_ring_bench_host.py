@@ -77,3 +77,27 @@ def test_rehearsal_roofline_never_above_one():
 def test_bench_failure_is_nonzero_exit():
     e = rb.BenchFailure("x")
     assert isinstance(e, SystemExit) and e.code == "x"  # a non-int code exits with status 1
+
+
+def test_channel_options_double_the_rings_on_distinct_gpus(monkeypatch):
+    """Distinct GPUs: the autotune times the default channel count and twice
+    it (bytes in flight per link grow with channels, not lanes); ranks
+    sharing one GPU keep the default (co-residency)."""
+    monkeypatch.delenv("MCCS_CHANNELS", raising=False)
+    assert rb.channel_options(C, 2, False) == [None, 8]
+    assert rb.channel_options(C, 4, False) == [None, 12]
+    assert rb.channel_options(C, 8, False) == [None, 14]
+    assert rb.channel_options(C, 8, True) == [None]
+    monkeypatch.setenv("MCCS_CHANNELS", "7")
+    assert rb.channel_options(C, 8, False) == [None]
+
+
+def test_candidates_stay_within_coresident_workgroups():
+    cands = rb._candidates(C, [None, 16, 32], [C.LOCALITY_RECEIVER], [None, 14])
+    tags = [t for t, _ in cands]
+    assert tags == ["receiver/lanes=auto", "receiver/lanes=16", "receiver/lanes=32",
+                    "receiver/lanes=auto/channels=14", "receiver/lanes=16/channels=14"]
+    for _, modes in cands:
+        for _, cfg in modes:
+            if cfg.channel_count and cfg.lanes:
+                assert cfg.channel_count * cfg.lanes <= rb.MAX_RING_WORKGROUPS
