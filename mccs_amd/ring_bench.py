@@ -612,7 +612,10 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
     cpu = None
     if not getattr(args, "no_cpu_baseline", False):
         cpu = cpu_sum_baseline(world, nbytes)
-        extras["cpu_ring_baseline"] = cpu_ring_baseline(world, min(nbytes, 16 << 20), info["channels"])
+        # host threads = world x channels: at most the default channel count
+        # (a doubled-channel transport would double the spinning threads)
+        host_ch = min(info["channels"], len(C.default_rings(world, 0)))
+        extras["cpu_ring_baseline"] = cpu_ring_baseline(world, min(nbytes, 16 << 20), host_ch)
     dist.barrier()
     prof = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()}
     return ring_line(world=world, steps=K, warmup=args.warmup, per_step_s=per_step, nbytes=nbytes, dt_name=dt_name,
