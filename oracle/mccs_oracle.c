@@ -316,6 +316,93 @@ int oracle_ring_allreduce(int dtype, int op, int nranks, const void *const *inpu
   return rc ? rc : (c.err ? -3 : 0);
 }
 
+/* ---------------- the same ring result, chunk-parallel ------------------- */
+/* For the BASELINE sizes (8 x 1 GiB fp16 = 4 Gi element-ops): the chunks of
+ * the walk are disjoint, and each chunk's value depends only on the inputs at
+ * its own offsets, so chunks may be evaluated in any order on any thread.
+ * Writes the common result of every rank into `output`, which must not
+ * overlap any input (no snapshot is taken).  Elements of the walk in
+ * [lo, hi) only when hi > lo (hi = 0: all). */
+struct walk_rec { int bid, chunk; long long offset, nelem; };
+struct walk_list { struct walk_rec *v; size_t n, cap; long long lo, hi; int err; };
+
+static void collect_visit(void *vctx, int bid, int chunk, long long offset, long long nelem) {
+  struct walk_list *w = (struct walk_list *)vctx;
+  if (nelem <= 0 || w->err) return;
+  if (w->hi > w->lo) { /* clip to [lo, hi) */
+    long long a = offset > w->lo ? offset : w->lo, b = offset + nelem < w->hi ? offset + nelem : w->hi;
+    if (b <= a) return;
+    offset = a; nelem = b - a;
+  }
+  if (w->n == w->cap) {
+    size_t cap = w->cap ? 2 * w->cap : 1024;
+    struct walk_rec *v = (struct walk_rec *)realloc(w->v, cap * sizeof *v);
+    if (!v) { w->err = 1; return; }
+    w->v = v; w->cap = cap;
+  }
+  w->v[w->n++] = (struct walk_rec){bid, chunk, offset, nelem};
+}
+
+struct mt_ring_job {
+  struct ring_ctx c; /* per-thread copy; c.outputs[0] is the single output */
+  const struct walk_list *w;
+  size_t first, step;
+};
+
+static void *mt_ring_worker(void *arg) {
+  struct mt_ring_job *j = (struct mt_ring_job *)arg;
+  struct ring_ctx *c = &j->c;
+  const int n = c->nranks;
+  for (size_t i = j->first; i < j->w->n && !c->err; i += j->step) {
+    const struct walk_rec *r = &j->w->v[i];
+    const size_t off = (size_t)r->offset * c->es, bytes = (size_t)r->nelem * c->es;
+    char *acc = (char *)c->outputs[0] + off;
+    /* the order of ring_visit: acc = x[idx chunk+1]; acc = fn(x[idx chunk+j], acc) */
+    memcpy(acc, (const char *)c->inputs[rank_at_index(c, r->bid, r->chunk + 1)] + off, bytes);
+    for (int k = 2; k <= n; ++k) {
+      const char *x = (const char *)c->inputs[rank_at_index(c, r->bid, r->chunk + k)] + off;
+      if (oracle_apply(c->dtype, c->op, acc, x, acc, (size_t)r->nelem)) c->err = 1;
+    }
+  }
+  return NULL;
+}
+
+int oracle_ring_allreduce_mt(int dtype, int op, int nranks, const void *const *inputs, void *output,
+                             size_t count, int nchannels, int nthreads_ref, int buff_size,
+                             const int *ring_orders, long long lo, long long hi, int nthreads) {
+  if (dtype < 0 || dtype >= T_NUM || op < 0 || op >= OP_NUM || nranks < 2) return -1;
+  struct walk_list w;
+  memset(&w, 0, sizeof w);
+  w.lo = lo; w.hi = hi;
+  int rc = oracle_ring_walk(count, nranks, nchannels, nthreads_ref, buff_size, (int)kElemSize[dtype],
+                            collect_visit, &w);
+  if (rc || w.err) { free(w.v); return rc ? rc : -2; }
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  struct mt_ring_job *jobs = (struct mt_ring_job *)calloc((size_t)nthreads, sizeof *jobs);
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof *th);
+  void *outs[1] = {output};
+  if (!jobs || !th) { free(jobs); free(th); free(w.v); return -2; }
+  for (int t = 0; t < nthreads; ++t) {
+    struct ring_ctx *c = &jobs[t].c;
+    c->dtype = dtype; c->op = op; c->nranks = nranks; c->es = kElemSize[dtype];
+    c->inputs = inputs; c->outputs = outs; c->ring_orders = ring_orders;
+    jobs[t].w = &w; jobs[t].first = (size_t)t; jobs[t].step = (size_t)nthreads;
+    if (t && pthread_create(&th[t], NULL, mt_ring_worker, &jobs[t]) != 0) {
+      mt_ring_worker(&jobs[t]);
+      th[t] = 0;
+    }
+  }
+  mt_ring_worker(&jobs[0]);
+  int err = jobs[0].c.err;
+  for (int t = 1; t < nthreads; ++t) {
+    if (th[t]) pthread_join(th[t], NULL);
+    err |= jobs[t].c.err;
+  }
+  free(jobs); free(th); free(w.v);
+  return err ? -3 : 0;
+}
+
 /* AllGather (all_gather.h:7-79, byte-count semantics of the int8 kernel):
  * rank r's output holds every rank's input block at offset rank*count. */
 int oracle_ring_allgather(int nranks, const void *const *inputs, void *const *outputs, size_t nbytes) {

@@ -41,6 +41,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_task_schema.restype = None
         L.oracle_ring_allreduce.argtypes = [ci, ci, ci, P(vp), P(vp), sz, ci, ci, ci, P(ci), P(ci)]
         L.oracle_ring_allgather.argtypes = [ci, P(vp), P(vp), sz]
+        L.oracle_ring_allreduce_mt.argtypes = [ci, ci, ci, P(vp), vp, sz, ci, ci, ci, P(ci),
+                                               ctypes.c_longlong, ctypes.c_longlong, ci]
         L.oracle_half_to_float.argtypes = [ctypes.c_uint16]
         L.oracle_half_to_float.restype = ctypes.c_float
         L.oracle_float_to_half.argtypes = [ctypes.c_float]
@@ -108,6 +110,26 @@ def ring_allreduce(dtype: int, op: int, inputs: list[np.ndarray], nchannels: int
     )
     assert rc == 0, rc
     return (out[0], owner) if want_owner else out[0]
+
+
+def ring_allreduce_mt(dtype: int, op: int, inputs, nchannels: int, nthreads: int, buff_size: int = 1 << 22,
+                      ring_orders=None, workers: int = 16, out: np.ndarray | None = None) -> np.ndarray:
+    """ring_allreduce's result, chunks evaluated on `workers` threads (same
+    walk, same per-chunk order; for the BASELINE sizes).  `inputs` are
+    C-contiguous numpy arrays (not copied); `out` must not alias them."""
+    n = len(inputs)
+    for x in inputs:
+        assert x.flags.c_contiguous and x.size == inputs[0].size and x.dtype == inputs[0].dtype
+    if out is None:
+        out = np.empty_like(inputs[0])
+    ro = None
+    if ring_orders is not None:
+        flat = np.ascontiguousarray(np.asarray(ring_orders, dtype=np.int32).reshape(-1))
+        ro = flat.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    rc = lib().oracle_ring_allreduce_mt(dtype, op, n, _pa(inputs), out.ctypes.data, inputs[0].size, nchannels,
+                                        nthreads, buff_size, ro, 0, 0, workers)
+    assert rc == 0, rc
+    return out
 
 
 def ring_allgather(inputs: list[np.ndarray]) -> np.ndarray:

@@ -197,6 +197,42 @@ def test_ring_oracle_matches_fifo_simulation(orc, n, dtype, count, nch, nthr, ri
         assert np.array_equal(sims[r].view(np.uint8), got.view(np.uint8)), f"rank {r}"
 
 
+MT_CASES = [
+    # (n, dtype, count, nch, nthr, buff, rings): multi-loop walks with a partial
+    # last loop (its own realChunkSize), ring overrides, doubled channels
+    (8, F32, 7 * 8 * (1 << 17) + 12345, 7, 544, 1 << 20, "default7"),
+    (8, F16, 2 * 8 * (1 << 18) * 3 + 999, 2, 544, 1 << 20, None),
+    (8, F32, 14 * 8 * (1 << 15) + 77, 14, 544, 1 << 18, "default14"),
+    (5, BF16, 300007, 3, 288, 1 << 19, [[4, 1, 0, 3, 2]] * 3),
+    (4, I32, 99991, 2, 160, 1 << 20, None),
+]
+
+
+@pytest.mark.parametrize("n,dtype,count,nch,nthr,buff,rings", MT_CASES)
+def test_chunk_parallel_oracle_equals_serial(orc, n, dtype, count, nch, nthr, buff, rings):
+    """oracle_ring_allreduce_mt (the BASELINE-size checker) evaluates the same
+    walk chunk-parallel: identical bytes to the serial restatement."""
+    from mccs_amd import comm as C
+
+    if isinstance(rings, str):
+        base = C.default_rings(n, 0)
+        rings = (base * 2)[:nch]
+    npdt = orc.NP_DTYPE[dtype]
+    rng = np.random.default_rng(count)
+    if dtype == I32:
+        inputs = [rng.integers(-1 << 20, 1 << 20, count).astype(npdt) for _ in range(n)]
+    elif dtype == BF16:
+        inputs = [((rng.random(count, dtype=np.float32) * 2 - 1).view(np.uint32) >> 16).astype(np.uint16)
+                  for _ in range(n)]
+    else:
+        inputs = [(rng.random(count, dtype=np.float32) * 2 - 1).astype(npdt) for _ in range(n)]
+    want = orc.ring_allreduce(dtype, 0, inputs, nchannels=nch, nthreads=nthr, buff_size=buff, ring_orders=rings)
+    for workers in (1, 7):
+        got = orc.ring_allreduce_mt(dtype, 0, inputs, nchannels=nch, nthreads=nthr, buff_size=buff,
+                                    ring_orders=rings, workers=workers)
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), workers
+
+
 def test_ring_order_matters_for_fp16(orc):
     """Sanity: the per-hop fp16 rounding is visible (a plain sum would differ)."""
     n = 8
