@@ -1,0 +1,413 @@
+"""Reference-driven launches ("depth A" of the drop-in).
+
+The reference's Rust service builds every device structure itself and calls
+the kernel by symbol.  This module restates exactly that
+host side for the reference-named kernels of libmccs_hip.so, with no
+communicator of this library involved, so the number an UNCHANGED service
+gets can be timed and its results checked:
+
+* transport/shm/transporter.rs:49-183 + transport/meta.rs:7-67 (the SHM
+  connector): per channel a 4096-byte SendBufMeta (head at offset 0), a
+  4096-byte RecvBufMeta (tail at offset 0) and one FIFO of buffer_size bytes
+  (8 slots of buffer_size/8).  Head lives with the sender, tail with the
+  receiver; the FIFO data with the sender (`Locality::Sender`, the reference
+  default) or with the receiver (`mccs.toml [shm] locality`).  Here the
+  memory is device memory of the owning GPU, shared with the peers over IPC
+  -- the xGMI connector that replaces the host-pinned SHM buffers (§8(f) 2);
+* comm/device.rs:35-183 (CommDevResources::new, conn_info_to_dev):
+  mccsDevCommAndChannels, per-channel peers arrays, userRanks,
+  ring prev/next/index, abortFlag, workFifoDone (host-mapped,
+  device.rs:56-64);
+* plan.rs:172-302 (compute_coll_work, select_best_channels: least-loaded
+  channels first), plan.rs:380-541 (wait_work_queue, upload_work: the
+  host-mapped work ring, wrap to the ring start, isLast / inFifo /
+  doneAcks, rolling acks), plan.rs:602-669 (get_task_schema, launch_plan:
+  grid = #channels, block = nthreads, e.g. 544).
+
+The launch goes through mccs_hip_launch_coll (the kernel symbol plus
+hipLaunchKernel, the call plan.rs:659-666 makes with cudaLaunchKernel).
+The reference-named kernels run the reference hand-off policy (system-scope
+release/acquire, 2-step slices, 8 FIFO slots, 30 s watchdog on abortFlag).
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+
+from . import _lib as L
+from . import abi
+
+FUNC_ALLREDUCE = 4  # mccsFuncAllReduce
+META = 4096  # SendBufMeta / RecvBufMeta, each padded to a page (meta.rs:7-67)
+WORK_DEPTH = 1024  # entries of the host-mapped work ring (power of two; the reference has 65536)
+ESIZE = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2}
+
+_hip = None
+
+
+def hip() -> ctypes.CDLL:
+    global _hip
+    if _hip is None:
+        h = ctypes.CDLL("libamdhip64.so")
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        h.hipHostMalloc.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_uint]
+        h.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_uint]
+        h.hipHostFree.argtypes = [vp]
+        h.hipMemcpy.argtypes = [vp, vp, sz, ctypes.c_int]
+        h.hipMemset.argtypes = [vp, ctypes.c_int, sz]
+        h.hipMalloc.argtypes = [ctypes.POINTER(vp), sz]
+        h.hipFree.argtypes = [vp]
+        h.hipSetDevice.argtypes = [ctypes.c_int]
+        _hip = h
+    return _hip
+
+
+def _ok(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what}: hipError {rc}")
+
+
+def _rolling_less(a: int, b: int) -> bool:
+    """plan.rs:695-704 rolling_less_u32."""
+    return ((a - b) & 0xFFFFFFFF) >= 0x80000000
+
+
+def _rolling_min(a: int, b: int) -> int:
+    return a if _rolling_less(a, b) else b
+
+
+def reference_rings(n: int, nch: int) -> list[list[int]]:
+    """proxy/engine.rs:296-320 default: ring 0 -> 1 -> ... -> n-1 on every channel."""
+    return [list(range(n)) for _ in range(nch)]
+
+
+class RefDrivenRank:
+    """One rank's device structures, built as the Rust service builds them.
+
+    `allgather(obj) -> list` exchanges picklable objects between the ranks
+    (torch.distributed.all_gather_object over gloo in the bench).  `rings`:
+    one send order per channel (comm_patterns_override, config.rs:32-47);
+    default the reference ring on every channel."""
+
+    def __init__(self, rank: int, n: int, device: int, allgather, nch: int = 2, rings=None,
+                 buff_size: int = 1 << 22, locality: str = "sender"):
+        if not 2 <= n or not 1 <= nch <= abi.MCCS_MAX_NCHANNELS or locality not in ("sender", "receiver"):
+            raise ValueError("bad reference-driven configuration")
+        self.rank, self.n, self.device, self.nch, self.buff = rank, n, device, nch, buff_size
+        self.rings = [list(r) for r in (rings or reference_rings(n, nch))]
+        if len(self.rings) != nch or any(sorted(r) != list(range(n)) for r in self.rings):
+            raise ValueError("each channel needs a ring over every rank")
+        self.locality = locality
+        self.lib = L.load()
+        h = hip()
+        _ok(h.hipSetDevice(device), "hipSetDevice")
+        self._dev_allocs, self._host_allocs, self._opened = [], [], []
+        # -- connector memory: [SendBufMeta][RecvBufMeta][FIFO] per channel, one allocation
+        self.stride = 2 * META + buff_size
+        mine, handle = ctypes.c_void_p(), (ctypes.c_char * 64)()
+        L.check(self.lib.mccsMemAllocShared(device, self.stride * nch, ctypes.byref(mine), handle),
+                "mccsMemAllocShared")
+        self._mine = mine.value
+        _ok(h.hipMemset(self._mine, 0, self.stride * nch), "hipMemset")
+        handles = allgather(bytes(handle))
+        self.base = [0] * n
+        for r in range(n):
+            if r == rank:
+                self.base[r] = self._mine
+                continue
+            p = ctypes.c_void_p()
+            L.check(self.lib.mccsMemOpenShared(device, handles[r], ctypes.byref(p)), "mccsMemOpenShared")
+            self.base[r] = p.value
+            self._opened.append(p.value)
+        # -- host-mapped sync: work ring + workFifoDone (device.rs:56-64)
+        self.h_work, self.d_work = self._host_mapped(abi.MCCS_WORK_SIZE * WORK_DEPTH)
+        self.h_done, self.d_done = self._host_mapped(4 * abi.MCCS_MAX_NCHANNELS)
+        ctypes.memset(self.h_done, 0, 4 * abi.MCCS_MAX_NCHANNELS)
+        self.d_abort = self._dev_alloc(64)
+        _ok(h.hipMemset(self.d_abort, 0, 64), "hipMemset")  # the reference leaves it uninitialised
+        # -- mccsDevCommAndChannels (device.rs:81-183)
+        hc = abi.mccsDevCommAndChannels()
+        hc.comm.rank, hc.comm.nRanks = rank, n
+        hc.comm.buffSizes[0] = buff_size
+        hc.comm.abortFlag = self.d_abort
+        self.d_peers = []
+        for c in range(nch):
+            ring = self.rings[c]
+            pos = ring.index(rank)
+            user_ranks = [ring[(pos + i) % n] for i in range(n)]
+            prev, nxt = user_ranks[n - 1], user_ranks[1]
+            peers = (abi.mccsDevChannelPeer * n)()
+            s = peers[nxt].send[0]
+            s.buffs[0] = self._fifo(c, rank if locality == "sender" else nxt)
+            s.head = self._send_meta(c, rank)
+            s.tail = self._recv_meta(c, nxt)
+            rv = peers[prev].recv[0]
+            rv.buffs[0] = self._fifo(c, prev if locality == "sender" else rank)
+            rv.tail = self._recv_meta(c, rank)
+            rv.head = self._send_meta(c, prev)
+            ch = hc.channels[c]
+            ch.peers = self._upload(bytes(peers))
+            self.d_peers.append(ch.peers)
+            ch.ring.prev, ch.ring.next = prev, nxt
+            ch.ring.userRanks = self._upload(b"".join(int(u).to_bytes(4, "little", signed=True) for u in user_ranks))
+            ch.ring.index = (pos - ring.index(0)) % n  # engine.rs:274-286
+            ch.workFifoDone = self.d_done + 4 * c
+        self.d_comm = self._upload(bytes(hc))
+        # -- planner state (plan.rs)
+        self.load = [0] * nch
+        self.next_available = 0
+        self.chan_next = [0] * nch
+        self.acked_min = 0
+        self.launches = 0
+        self._works = {}
+
+    # memory helpers ---------------------------------------------------------
+    def _fifo(self, c, r):
+        return self.base[r] + c * self.stride + 2 * META
+
+    def _send_meta(self, c, r):
+        return self.base[r] + c * self.stride
+
+    def _recv_meta(self, c, r):
+        return self.base[r] + c * self.stride + META
+
+    def _host_mapped(self, nbytes):
+        hp, dp = ctypes.c_void_p(), ctypes.c_void_p()
+        _ok(hip().hipHostMalloc(ctypes.byref(hp), nbytes, 0x2), "hipHostMalloc(mapped)")
+        self._host_allocs.append(hp.value)
+        _ok(hip().hipHostGetDevicePointer(ctypes.byref(dp), hp, 0), "hipHostGetDevicePointer")
+        return hp.value, dp.value
+
+    def _dev_alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        _ok(hip().hipMalloc(ctypes.byref(p), nbytes), "hipMalloc")
+        self._dev_allocs.append(p.value)
+        return p.value
+
+    def _upload(self, b: bytes) -> int:
+        p = self._dev_alloc(len(b))
+        buf = ctypes.create_string_buffer(b, len(b))
+        _ok(hip().hipMemcpy(p, buf, len(b), 1), "hipMemcpy H2D")
+        return p
+
+    # plan.rs ---------------------------------------------------------------
+    def _wait_work_queue(self, target: int, timeout_s: float = 60.0) -> None:
+        """plan.rs:380-422."""
+        if not _rolling_less((self.acked_min + WORK_DEPTH) & 0xFFFFFFFF, target & 0xFFFFFFFF):
+            return
+        done = (ctypes.c_uint32 * abi.MCCS_MAX_NCHANNELS).from_address(self.h_done)
+        t0 = time.monotonic()
+        while True:
+            ackd = list(done)
+            ackd_all = self.next_available
+            for c in range(self.nch):
+                if ackd[c] != self.chan_next[c]:
+                    ackd_all = _rolling_min(ackd_all, ackd[c])
+            for c in range(self.nch):
+                if ackd[c] == self.chan_next[c]:
+                    done[c] = ackd_all
+            self.acked_min = ackd_all
+            if not _rolling_less((self.acked_min + WORK_DEPTH) & 0xFFFFFFFF, target & 0xFFFFFFFF):
+                return
+            if time.monotonic() - t0 > timeout_s:
+                raise RuntimeError("reference-driven work ring: no acknowledgement (kernel stuck?)")
+            time.sleep(0)
+
+    def all_reduce(self, send_ptr: int, recv_ptr: int, count: int, dtype: int, op: int, stream: int) -> None:
+        """One AllReduce task through plan.rs's path (one work element per
+        selected channel), launched on `stream`."""
+        nbytes = count * ESIZE[dtype]
+        sch, nthr = ctypes.c_int(), ctypes.c_int()
+        self.lib.mccs_task_schema(nbytes, self.nch, ctypes.byref(sch), ctypes.byref(nthr))
+        k, nthr = sch.value, nthr.value
+        # select_best_channels (plan.rs:292-302): least loaded first; blocks
+        # map to the set bits of channelMask in ascending channel order
+        chans = sorted(sorted(range(self.nch), key=lambda i: (self.load[i], i))[:k])
+        for c in chans:
+            self.load[c] += nbytes
+        mask_q = WORK_DEPTH - 1
+        start = self.next_available
+        if ((start + k - 1) & mask_q) < (start & mask_q):  # wrap to the ring start
+            start = (start + mask_q) & ~mask_q & 0xFFFFFFFF
+            self.next_available = start
+        self._wait_work_queue(start + k)
+        acks = (start + k + 1) & 0xFFFFFFFF
+        key = (send_ptr, recv_ptr, count, k, nthr)
+        works = self._works.get(key)
+        if works is None:  # work_elem_conversion (plan.rs:550-600), built once per shape
+            works = []
+            for nth in range(k):
+                w = abi.mccsDevWork()
+                w.header.type = 1  # mccsDevWorkTypeColl
+                w.header.isLast, w.header.inFifo = 1, 1
+                e = w.elems[0]
+                e.isUsed, e.nWarps = 1, nthr // 32
+                e.sendbuff, e.recvbuff, e.count = send_ptr, recv_ptr, count
+                e.bid, e.nChannels = nth, k
+                works.append(w)
+            if len(self._works) > 64:
+                self._works.clear()
+            self._works[key] = works
+        for nth, c in enumerate(chans):
+            w = works[nth]
+            w.header.doneAcks = acks
+            ctypes.memmove(self.h_work + ((start + nth) & mask_q) * abi.MCCS_WORK_SIZE, ctypes.addressof(w),
+                           abi.MCCS_WORK_SIZE)
+            self.chan_next[c] = acks
+        self.next_available = (start + k) & 0xFFFFFFFF
+        channel_mask = 0
+        for c in chans:
+            channel_mask |= 1 << c
+        rc = self.lib.mccs_hip_launch_coll(FUNC_ALLREDUCE, dtype, op, self.d_comm, channel_mask,
+                                           self.d_work + (start & mask_q) * abi.MCCS_WORK_SIZE, k, nthr, stream)
+        L.check(rc, "mccs_hip_launch_coll")
+        self.launches += 1
+        self.last_plan = (k, nthr, [self.rings[c] for c in chans])
+
+    def aborted(self) -> bool:
+        v = ctypes.c_int32()
+        _ok(hip().hipMemcpy(ctypes.byref(v), self.d_abort, 4, 2), "hipMemcpy D2H")
+        return v.value != 0
+
+    def steps(self) -> list[int]:
+        """conn->step of this rank's send and recv connectors, per channel."""
+        out = []
+        for c in range(self.nch):
+            ring = self.rings[c]
+            pos = ring.index(self.rank)
+            pr = (abi.mccsDevChannelPeer * self.n)()
+            _ok(hip().hipMemcpy(ctypes.byref(pr), self.d_peers[c], ctypes.sizeof(pr), 2), "hipMemcpy D2H")
+            out += [int(pr[ring[(pos + 1) % self.n]].send[0].step), int(pr[ring[(pos - 1) % self.n]].recv[0].step)]
+        return out
+
+    def done_acks(self) -> list[int]:
+        return list((ctypes.c_uint32 * abi.MCCS_MAX_NCHANNELS).from_address(self.h_done))[:self.nch]
+
+    def close(self, barrier=None) -> None:
+        """Unmaps the peers' memory; `barrier()` (all ranks) before freeing our
+        own, which the peers may still have mapped."""
+        h = hip()
+        h.hipDeviceSynchronize()
+        for p in self._opened:
+            self.lib.mccsMemCloseShared(self.device, ctypes.c_void_p(p))
+        self._opened = []
+        if barrier is not None:
+            barrier()
+        if self._mine:
+            self.lib.mccsMemFreeShared(self.device, ctypes.c_void_p(self._mine))
+            self._mine = 0
+        for p in self._dev_allocs:
+            h.hipFree(ctypes.c_void_p(p))
+        for p in self._host_allocs:
+            h.hipHostFree(ctypes.c_void_p(p))
+        self._dev_allocs, self._host_allocs = [], []
+
+
+# ---------------------------------------------------------------------------
+# Timing harness shared by bench.py (config.reference_driven, N > 1) and
+# tools/refdrv_bench.py (the 2-process rehearsal on one GPU).
+
+def exact_inputs(torch, count: int, rank: int, dtype, device):
+    """Values k/64 with |k| <= 127: every partial sum of <= 8 ranks is exact
+    in fp16 and fp32, so the result is independent of the summation order."""
+    i = torch.arange(count, dtype=torch.int64, device=device)
+    return (((i * 7 + rank * 13) % 255) - 127).to(torch.float32).div_(64.0).to(dtype)
+
+
+def expected_exact(torch, count: int, world: int, dtype, device):
+    acc = torch.zeros(count, dtype=torch.float64, device=device)
+    for r in range(world):
+        acc += exact_inputs(torch, count, r, torch.float64, device)
+    return acc.to(dtype)
+
+
+def default_variants(world: int, default_rings) -> list[dict]:
+    """The configurations an unchanged service can run by configuration alone:
+    mccs.toml's channel_count = 2 (the shipped default), MCCS_MAX_NCHANNELS =
+    32 on the reference ring, and the same 32-channel budget over this
+    library's link-spreading rings given as comm_patterns_override, with the
+    FIFO data at the sender (the reference SHM layout) or the receiver."""
+    base = default_rings(world, 0)
+    uniq = []
+    for r in base:
+        if r not in uniq:
+            uniq.append(r)
+    spread = (uniq * 32)[:(32 // len(uniq)) * len(uniq)]
+    return [
+        {"name": "ch2_reference_ring_sender", "nch": 2, "rings": None, "locality": "sender"},
+        {"name": "ch32_reference_ring_sender", "nch": 32, "rings": None, "locality": "sender"},
+        {"name": f"ch{len(spread)}_spread_rings_sender", "nch": len(spread), "rings": spread, "locality": "sender"},
+        {"name": f"ch{len(spread)}_spread_rings_receiver", "nch": len(spread), "rings": spread,
+         "locality": "receiver"},
+    ]
+
+
+def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbytes: int, variants: list[dict],
+                          warmup: int = 3, steps: int = 10, group=None) -> list[dict]:
+    """Times every variant at `nbytes` fp32 per rank (algbw = nbytes / t per
+    AllReduce, max over ranks), each gated by an exact-sum check on every
+    rank.  Ranks must be one per process; `dist` carries the handle exchange
+    and barriers (gloo)."""
+    dtype, code = torch.float32, 7
+    count = nbytes // 4
+    dev = torch.device("cuda", device)
+    send = exact_inputs(torch, count, rank, dtype, dev)
+    want = expected_exact(torch, count, world, dtype, dev)
+    recv = torch.empty_like(send)
+    stream = torch.cuda.Stream(device=dev)
+
+    def allgather(obj):
+        out = [None] * world
+        dist.all_gather_object(out, obj, group=group)
+        return out
+
+    def barrier():
+        dist.barrier(group=group)
+
+    def max_over_ranks(v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return float(t.item())
+
+    out = []
+    for v in variants:
+        res = {"variant": v["name"], "channels": v["nch"], "locality": v["locality"]}
+        rr = None
+        try:
+            rr = RefDrivenRank(rank, world, device, allgather, nch=v["nch"], rings=v["rings"],
+                               locality=v["locality"])
+            barrier()
+            recv.zero_()
+            torch.cuda.synchronize(dev)
+            rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+            stream.synchronize()
+            k, nthr, _ = rr.last_plan
+            ok = bool(torch.equal(recv, want)) and not rr.aborted()
+            ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
+            res.update(grid=k, block=nthr, exact=ok)
+            if ok:
+                for _ in range(warmup):
+                    rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+                stream.synchronize()
+                barrier()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+                stream.synchronize()
+                el = max_over_ranks(time.perf_counter() - t0)
+                ok2 = bool(torch.equal(recv, want)) and not rr.aborted()
+                ok2 = max_over_ranks(0.0 if ok2 else 1.0) == 0.0
+                ms = el / steps * 1e3
+                res.update(ms_per_allreduce=round(ms, 4), algbw_GBps=round(nbytes / (ms * 1e-3) / 1e9, 2),
+                           busbw_GBps=round(nbytes / (ms * 1e-3) / 1e9 * 2 * (world - 1) / world, 2),
+                           exact_after_timing=ok2, steps=steps)
+        except Exception as e:  # recorded, never fatal to the caller's line
+            res["error"] = f"{type(e).__name__}: {e}"[:300]
+        finally:
+            if rr is not None:
+                try:
+                    rr.close(barrier)
+                except Exception as e:
+                    res.setdefault("error", f"close: {e}"[:300])
+        out.append(res)
+    return out
