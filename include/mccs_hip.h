@@ -92,7 +92,10 @@ const void *mccs_hip_coll_kernel(int func, int dtype, int op);
  * this function by this process, is still running, the call is refused with
  * mccsInvalidUsage and nothing is launched.  Co-located ranks go through the
  * communicator API (mccsCommInitAll + mccsGroupStart/End), which fuses them
- * into one launch. */
+ * into one launch.  The reference-named kernels run the reference FIFO depth
+ * (MCCS_BUFFER_SLOTS = 8 slots per connection): a communicator of this library
+ * built with another fifo_slots is refused with mccsInvalidUsage (its peers
+ * would index a different slot ring). */
 mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, struct mccsDevComm *comm, uint64_t channelMask,
                                   struct mccsDevWork *workHead, unsigned grid, unsigned block,
                                   hipStream_t stream);
@@ -103,16 +106,23 @@ typedef struct mccsComm *mccsComm_t;
 #define MCCS_LOCALITY_RECEIVER 1 /* FIFO data in the receiver's HBM; sender writes over xGMI */
 #define MCCS_FIFO_UNCACHED 0     /* hipDeviceMallocUncached arena: no L2 maintenance needed */
 #define MCCS_FIFO_DEVICE 1       /* hipMalloc arena + system-scope release/acquire */
+#define MCCS_FIFO_UNCACHED_RELEASE 2 /* uncached arena + a system-scope release fence before every
+                                        post (the reference's __threadfence_system before postPeer,
+                                        prims_simple.h:120-125,211); polls stay relaxed */
 
 /* Communicator profile: comm_default_config (mccs.toml:18-20, config.rs:15-97)
- * plus the MI355X execution knobs.  Zero fields take defaults. */
+ * plus the MI355X execution knobs.  Zero fields take defaults.
+ * ABI note: `fifo_slots` was appended in library version 0.3, which grew the
+ * struct; mccsCommConfigDefault() writes sizeof(mccsCommConfig) bytes, so a
+ * caller compiled against an older header must be rebuilt.  Callers binding
+ * the struct by hand (ctypes, bindgen) check mccsCommConfigSize(). */
 typedef struct {
   int channel_count;    /* rings; 0 = auto: 2 x edge-disjoint Hamiltonian cycles of the node */
   int buffer_size;      /* FIFO bytes per connection (buffer_sizes[0]); 0 = 4 MiB */
   int lanes;            /* workgroups per channel; 0 = auto (64 / channels, <= 64, fitted to residency) */
-  int block_threads;    /* threads per workgroup (64..576, multiple of 32); 0 = 512 */
+  int block_threads;    /* threads per workgroup (96..576, multiple of 32); 0 = MCCS_RING_MAX_THREADS (576) */
   int locality;         /* MCCS_LOCALITY_*; default RECEIVER (remote writes; SENDER = reference shm layout) */
-  int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED */
+  int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED (MCCS_FIFO_MEMORY=uncached|release|device) */
   int timeout_ms;       /* FIFO spin watchdog; 0 = 30000, < 0 = never */
   int work_fifo_depth;  /* mccsDevWork slots (power of two); 0 = 4096 */
   int bridge_streams;   /* -1 (default): launch on the caller's stream; 1: user stream -> comm stream -> user stream events (libmccs two-stream bridge) */
@@ -124,6 +134,8 @@ typedef struct {
 } mccsCommConfig;
 
 void mccsCommConfigDefault(mccsCommConfig *cfg);
+/* sizeof(mccsCommConfig) as this library was built (see the ABI note above). */
+size_t mccsCommConfigSize(void);
 
 /* One process drives `nranks` ranks (the reference service model: one mccs
  * process owns every GPU of the host).  devices[r] is rank r's GPU; devices
@@ -159,7 +171,8 @@ mccsResult_t mccsCommSync(mccsComm_t comm);
 /* Raises the comm's abortFlag: in-flight kernels exit at their next poll. */
 mccsResult_t mccsCommAbort(mccsComm_t comm);
 mccsResult_t mccsCommDestroy(mccsComm_t comm);
-/* rank, nranks, device, channels, lanes, block threads, fifo memory kind. */
+/* rank, nranks, device, channels, lanes, block threads, fifo memory kind
+ * (MCCS_FIFO_*: the hand-off mode the comm's launches run). */
 mccsResult_t mccsCommInfo(mccsComm_t comm, int *info7);
 /* ring send order of channel ch (nranks ints). */
 mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int *order);

@@ -90,6 +90,7 @@ SIGNATURES: dict[str, tuple] = {
         _c_int, [_c_int, _c_int, _c_int, _c_void_p, ctypes.c_uint64, _c_void_p, ctypes.c_uint, ctypes.c_uint,
                  _c_void_p]),
     "mccsCommConfigDefault": (None, [_P(_CommConfig)]),
+    "mccsCommConfigSize": (_c_size_t, []),
     "mccsCommInitAll": (_c_int, [_P(_c_void_p), _c_int, _P(_c_int), _P(_CommConfig)]),
     "mccsConnectHandleSize": (_c_size_t, []),
     "mccsCommSetupRank": (_c_int, [_P(_c_void_p), _c_int, _c_int, _c_int, _P(_CommConfig), _c_void_p]),
@@ -143,6 +144,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mccsCommConfigSize() != ctypes.sizeof(_CommConfig):  # the struct grew once (mccs_hip.h ABI note)
+        raise RuntimeError(f"{p}: mccsCommConfig is {lib.mccsCommConfigSize()} bytes, this binding "
+                           f"{ctypes.sizeof(_CommConfig)}: rebuild or update mccs_amd/_lib.py")
     _lib = lib
     return lib
 

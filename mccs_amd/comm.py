@@ -59,7 +59,9 @@ class AllReduceOpType(enum.IntEnum):
 
 
 LOCALITY_SENDER, LOCALITY_RECEIVER = 0, 1
-FIFO_UNCACHED, FIFO_DEVICE = 0, 1
+# MCCS_FIFO_*: uncached arena (relaxed hand-offs), plain device arena
+# (system-scope release/acquire), uncached arena + release fence before posts
+FIFO_UNCACHED, FIFO_DEVICE, FIFO_UNCACHED_RELEASE = 0, 1, 2
 
 
 @dataclass

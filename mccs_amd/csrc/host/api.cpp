@@ -62,7 +62,9 @@ static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
   if (c.channel_count < 0 || c.channel_count > MCCS_MAX_NCHANNELS) return mccsInvalidArgument;
   if (c.work_fifo_depth & (c.work_fifo_depth - 1)) return mccsInvalidArgument;
   if (c.locality != MCCS_LOCALITY_SENDER && c.locality != MCCS_LOCALITY_RECEIVER) return mccsInvalidArgument;
-  if (c.fifo_memory != MCCS_FIFO_UNCACHED && c.fifo_memory != MCCS_FIFO_DEVICE) return mccsInvalidArgument;
+  if (c.fifo_memory != MCCS_FIFO_UNCACHED && c.fifo_memory != MCCS_FIFO_DEVICE &&
+      c.fifo_memory != MCCS_FIFO_UNCACHED_RELEASE)
+    return mccsInvalidArgument;
   if (nranks < 1 || nranks > 64) return mccsInvalidArgument;
   if (c.fifo_slots != 8 && c.fifo_slots != 16 && c.fifo_slots != 32) return mccsInvalidArgument;
   return mccsSuccess;
@@ -188,7 +190,9 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BRIDGE_STREAMS")) cfg->bridge_streams = std::atoi(v);
   if (const char* v = std::getenv("MCCS_FIFO_MEMORY"))
-    cfg->fifo_memory = (v[0] == 'd' || v[0] == 'D') ? MCCS_FIFO_DEVICE : MCCS_FIFO_UNCACHED;
+    cfg->fifo_memory = (v[0] == 'd' || v[0] == 'D')   ? MCCS_FIFO_DEVICE
+                       : (v[0] == 'r' || v[0] == 'R') ? MCCS_FIFO_UNCACHED_RELEASE
+                                                      : MCCS_FIFO_UNCACHED;
   if (const char* v = std::getenv("MCCS_BLOCK_THREADS")) cfg->block_threads = std::atoi(v);
   if (const char* v = std::getenv("MCCS_CHANNELS")) cfg->channel_count = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BUFFER_SIZE")) cfg->buffer_size = std::atoi(v);
@@ -216,11 +220,15 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
   for (int i = 0; i < nranks && r == mccsSuccess; ++i)
     for (int j = 0; j < nranks && r == mccsSuccess; ++j) r = enable_peer(devices[i], devices[j]);
   if (r == mccsSuccess) {
-    bool all_uc = true;
-    for (int i = 0; i < nranks; ++i) all_uc = all_uc && cs[i]->own_arena_uncached;
+    bool all_uc = true, release = false;
+    for (int i = 0; i < nranks; ++i) {
+      all_uc = all_uc && cs[i]->own_arena_uncached;
+      release = release || cs[i]->cfg.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
+    }
     for (int i = 0; i < nranks; ++i) {
       for (int j = 0; j < nranks; ++j) cs[i]->peer_arena[j] = cs[j]->own_arena;
       cs[i]->all_uncached = all_uc;
+      cs[i]->fifo_release = release;
     }
     for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_build_device(cs[i]);
   }
@@ -270,8 +278,13 @@ extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks,
   h.nranks = nranks;
   h.device = device;
   h.pid = (int32_t)getpid();
-  h.fifo_memory = c->own_arena_uncached ? MCCS_FIFO_UNCACHED : MCCS_FIFO_DEVICE;
+  h.fifo_memory = !c->own_arena_uncached                              ? MCCS_FIFO_DEVICE
+                  : c->cfg.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE ? MCCS_FIFO_UNCACHED_RELEASE
+                                                                     : MCCS_FIFO_UNCACHED;
   h.nch = c->nch;
+  h.lanes = c->lanes;
+  h.lanes_auto = c->cfg.lanes > 0 ? 0 : 1;
+  h.ring_cap = coresident_ring_blocks(c->block_threads, device);
   h.arena_bytes = c->layout.total();
   h.buffer_size = c->layout.buffer_size;
   gethostname(h.host, sizeof(h.host) - 1);
@@ -284,13 +297,42 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
   Comm* c = (Comm*)comm;
   if (!c || !all_handles || c->connected) return mccsInvalidUsage;
   const ConnectHandle* hs = (const ConnectHandle*)all_handles;
-  bool all_uc = true;
+  bool all_uc = true, release = false;
   for (int r = 0; r < c->nranks; ++r) {
     const ConnectHandle& h = hs[r];
     if (h.magic != kHandleMagic || h.rank != r || h.nranks != c->nranks || h.nch != c->nch ||
         h.arena_bytes != c->layout.total() || h.buffer_size != c->layout.buffer_size)
       return mccsInvalidArgument;  // ranks disagree on the communicator profile
-    all_uc = all_uc && h.fifo_memory == MCCS_FIFO_UNCACHED;
+    all_uc = all_uc && h.fifo_memory != MCCS_FIFO_DEVICE;
+    release = release || h.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
+    if (h.lanes != hs[0].lanes || h.lanes_auto != hs[0].lanes_auto) return mccsInvalidArgument;
+  }
+  // Ranks of this communicator that share a GPU as separate processes run
+  // separate launches that spin on each other's flags, so all of them must be
+  // resident together.  Unlike one fused launch (mccsCommInitAll), the GPU
+  // does not co-schedule separate processes' grids as a unit (4 processes x
+  // 60 workgroups = 240 of 256 slots timed out on MI355X), so automatic lanes
+  // shrink to half the slots; explicit lanes that cannot fit at all are
+  // refused instead of deadlocking.  Every rank derives the same lane count
+  // from the same handles (a connection's two ends must agree on lanes).
+  {
+    int max_share = 1, cap = 1 << 30;
+    for (int r = 0; r < c->nranks; ++r) {
+      int share = 0;
+      for (int q = 0; q < c->nranks; ++q)
+        share += hs[q].device == hs[r].device && std::strncmp(hs[q].host, hs[r].host, sizeof(hs[q].host)) == 0;
+      max_share = std::max(max_share, share);
+      if (hs[r].ring_cap > 0) cap = std::min(cap, (int)hs[r].ring_cap);
+    }
+    if (max_share > 1 && cap < (1 << 30)) {
+      if (hs[0].lanes_auto) {
+        const int fit = cap / 2 / (max_share * c->nch);
+        if (fit < 1) return mccsInvalidUsage;
+        c->lanes = std::min(c->lanes, fit);
+      } else if ((long)max_share * c->nch * c->lanes > cap) {
+        return mccsInvalidUsage;
+      }
+    }
   }
   DeviceGuard g(c->device);
   for (int r = 0; r < c->nranks; ++r) {
@@ -308,6 +350,7 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
     c->peer_opened_ipc[r] = true;
   }
   c->all_uncached = all_uc;
+  c->fifo_release = release;
   return comm_build_device(c);
 }
 
@@ -385,7 +428,7 @@ extern "C" mccsResult_t mccsCommInfo(mccsComm_t comm, int* info) {
   info[3] = c->nch;
   info[4] = c->lanes;
   info[5] = c->block_threads;
-  info[6] = c->all_uncached ? MCCS_FIFO_UNCACHED : MCCS_FIFO_DEVICE;
+  info[6] = !c->all_uncached ? MCCS_FIFO_DEVICE : c->fifo_release ? MCCS_FIFO_UNCACHED_RELEASE : MCCS_FIFO_UNCACHED;
   return mccsSuccess;
 }
 

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <mutex>
 
 #include "comm.h"
@@ -98,7 +99,7 @@ void default_rings(int n, int nch_req, std::vector<std::vector<int>>* rings) {
 // ---------------------------------------------------------------------------
 mccsResult_t comm_set_kernel_cfg(Comm* c) {
   mccsRingKernelCfg k{};
-  k.fence_mode = c->all_uncached ? MCCS_FENCE_UNCACHED : MCCS_FENCE_SYSTEM;
+  k.fence_mode = !c->all_uncached ? MCCS_FENCE_SYSTEM : c->fifo_release ? MCCS_FENCE_UNCACHED_RELEASE : MCCS_FENCE_UNCACHED;
   k.err_line = 1;  // d_abort is a 64-byte line of ours: errors go to its word 1
   k.fifo_slots = (uint32_t)c->cfg.fifo_slots;
   const int tmo = c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms;
@@ -146,6 +147,27 @@ static void pool_give(int device, bool uncached, size_t bytes, char* p) {
   g_pool.push_back(PooledArena{rt_generation(), device, uncached, bytes, p});
 }
 
+// A fake runtime's "device" memory dies with it (rt.cpp): its pooled arenas
+// must never be handed out again.  Real HIP arenas (generation 0) stay.
+void comm_pool_drop_generation(unsigned generation) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (size_t i = 0; i < g_pool.size();)
+    if (g_pool[i].generation == generation) g_pool.erase(g_pool.begin() + i);
+    else ++i;
+}
+
+// Live communicators' device structures -> their FIFO depth, so the external
+// launch (mccs_hip_launch_coll, whose reference-named kernels assume the
+// reference's 8 slots) can refuse a library communicator built with another.
+static std::mutex g_live_mu;
+static std::map<const void*, int> g_live_fifo_slots;
+
+int comm_fifo_slots_of(const void* d_comm) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  auto it = g_live_fifo_slots.find(d_comm);
+  return it == g_live_fifo_slots.end() ? 0 : it->second;
+}
+
 // Swap this comm's uncached arena for a plain device arena (used when IPC
 // export of the uncached one is refused).  The old range goes back to the pool.
 mccsResult_t comm_switch_to_device_arena(Comm* c) {
@@ -170,7 +192,7 @@ mccsResult_t comm_alloc_local(Comm* c) {
   const size_t bytes = c->layout.total();
   c->own_arena = nullptr;
   c->own_arena_uncached = false;
-  if (c->cfg.fifo_memory == MCCS_FIFO_UNCACHED) {
+  if (c->cfg.fifo_memory != MCCS_FIFO_DEVICE) {  // UNCACHED or UNCACHED_RELEASE
     c->own_arena = pool_take(c->device, true, bytes);
     if (c->own_arena) {
       c->own_arena_uncached = true;
@@ -291,6 +313,10 @@ mccsResult_t comm_build_device(Comm* c) {
   MCCS_HIP(rt().Memcpy(c->d_comm, &hc, sizeof(hc), hipMemcpyHostToDevice));
   MCCS_HIP(rt().Memcpy(c->d_view, views, sizeof(views), hipMemcpyHostToDevice));
   MCCS_CHECK(comm_set_kernel_cfg(c));
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live_fifo_slots[c->d_comm] = c->cfg.fifo_slots;
+  }
   c->connected = true;
   return mccsSuccess;
 }
@@ -322,6 +348,10 @@ mccsResult_t comm_make_event_ipc(Comm* c) {
 
 mccsResult_t comm_free(Comm* c) {
   DeviceGuard g(c->device);
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live_fifo_slots.erase(c->d_comm);
+  }
   // the last launch (any stream) must be done before its arenas are reused
   if (c->event) (void)rt().EventSynchronize(c->event);
   if (c->stream) (void)rt().StreamSynchronize(c->stream);

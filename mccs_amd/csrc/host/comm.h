@@ -79,7 +79,9 @@ struct ConnectHandle {
   int32_t pid;
   int32_t fifo_memory;
   int32_t nch;
-  int32_t pad;
+  int32_t lanes;       // this rank's lane count before the co-residency check
+  int32_t lanes_auto;  // 1: lanes came from the automatic rule (cfg.lanes == 0)
+  int32_t ring_cap;    // coresident_ring_blocks() of this rank's device
   uint64_t arena_bytes;
   uint64_t buffer_size;
   hipIpcMemHandle_t ipc;
@@ -113,6 +115,7 @@ struct Comm {
   std::vector<char*> peer_arena;
   std::vector<bool> peer_opened_ipc;
   bool all_uncached = true;
+  bool fifo_release = false;  // some rank asked for MCCS_FIFO_UNCACHED_RELEASE: release fence before posts
   // device resources (comm/device.rs)
   mccsDevCommAndChannels* d_comm = nullptr;
   std::vector<mccsDevChannelPeer*> d_peers;
@@ -164,6 +167,8 @@ mccsResult_t comm_free(Comm* c);
 mccsResult_t comm_set_kernel_cfg(Comm* c);
 mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream on first use
 mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one
+int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live library comm's device struct, else 0
+void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
 // plan.cpp
 mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count);
 mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams);

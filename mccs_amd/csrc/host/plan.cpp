@@ -381,7 +381,10 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       ma.comm[k] = (mccsDevComm*)ck->d_comm;
       ma.work[k] = lds[k].work;
       ma.view[k] = ck->d_view;
-      if (ck->kcfg.fence_mode != MCCS_FENCE_UNCACHED) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
+      // safest of the group: SYSTEM > UNCACHED_RELEASE > UNCACHED
+      if (ck->kcfg.fence_mode == MCCS_FENCE_SYSTEM) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
+      else if (ck->kcfg.fence_mode == MCCS_FENCE_UNCACHED_RELEASE && ma.cfg.fence_mode == MCCS_FENCE_UNCACHED)
+        ma.cfg.fence_mode = MCCS_FENCE_UNCACHED_RELEASE;
       ma.cfg.timeout_ticks = (ma.cfg.timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)
                                  ? 0
                                  : std::max(ma.cfg.timeout_ticks, ck->kcfg.timeout_ticks);

@@ -4,6 +4,7 @@
 #include "rt.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -259,20 +260,36 @@ class FakeRuntime final : public DeviceRuntime {
 };
 
 HipRuntime g_hip;
-std::unique_ptr<FakeRuntime> g_fake;
-unsigned g_generation = 0;
+// The installed fake (owned by g_fake_owner) is published through an atomic
+// pointer so rt() never reads a half-swapped unique_ptr; install / removal is
+// serialised by g_fake_mu.  Test-only contract: no communicator created under
+// one runtime is used or destroyed under another.
+std::mutex g_fake_mu;
+std::unique_ptr<FakeRuntime> g_fake_owner;
+std::atomic<FakeRuntime*> g_fake{nullptr};
+// 0 = the HIP runtime; every fake install gets a fresh nonzero id, so arenas
+// pooled under HIP stay reusable across fake install / remove cycles
+std::atomic<unsigned> g_generation{0};
+unsigned g_fake_serial = 0;
 
 }  // namespace
 
-DeviceRuntime& rt() { return g_fake ? (DeviceRuntime&)*g_fake : (DeviceRuntime&)g_hip; }
-
-void rt_use_fake(int ndevices) {
-  ++g_generation;
-  if (ndevices > 0) g_fake.reset(new FakeRuntime(ndevices));
-  else g_fake.reset();
+DeviceRuntime& rt() {
+  FakeRuntime* f = g_fake.load(std::memory_order_acquire);
+  return f ? (DeviceRuntime&)*f : (DeviceRuntime&)g_hip;
 }
 
-unsigned rt_generation() { return g_generation; }
+void rt_use_fake(int ndevices) {
+  std::lock_guard<std::mutex> lk(g_fake_mu);
+  const unsigned old = g_generation.load();
+  std::unique_ptr<FakeRuntime> next(ndevices > 0 ? new FakeRuntime(ndevices) : nullptr);
+  g_fake.store(next.get(), std::memory_order_release);
+  g_generation.store(ndevices > 0 ? ++g_fake_serial : 0u);
+  g_fake_owner.swap(next);  // the previous fake (if any) dies with `next` below
+  if (old != 0) comm_pool_drop_generation(old);  // its arenas were its host memory
+}
+
+unsigned rt_generation() { return g_generation.load(); }
 
 }  // namespace mccs
 
@@ -288,13 +305,15 @@ extern "C" mccsResult_t mccs_test_fake_runtime(int ndevices) {
 // Copies the fake runtime's event log (NUL-terminated, truncated to cap) and
 // optionally clears it; returns the log length, or -1 without a fake.
 extern "C" int mccs_test_fake_log(char* buf, int cap, int clear) {
-  if (!mccs::g_fake) return -1;
-  const std::string s = mccs::g_fake->log();
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  const std::string s = f->log();
   if (buf && cap > 0) {
     const size_t n = std::min(s.size(), (size_t)cap - 1);
     std::memcpy(buf, s.data(), n);
     buf[n] = '\0';
   }
-  if (clear) mccs::g_fake->clear();
+  if (clear) f->clear();
   return (int)s.size();
 }

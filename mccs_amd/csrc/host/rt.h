@@ -51,8 +51,9 @@ class DeviceRuntime {
 DeviceRuntime& rt();
 // Installs a recording fake with `ndevices` devices (0 restores HIP).
 void rt_use_fake(int ndevices);
-// Bumped by every rt_use_fake: memory pooled under one runtime is never
-// handed out under another.
+// Identity of the current runtime: 0 for HIP, a fresh nonzero id per
+// installed fake.  Memory pooled under one runtime is never handed out under
+// another; a removed fake's pooled arenas are dropped (its memory died with it).
 unsigned rt_generation();
 
 }  // namespace mccs

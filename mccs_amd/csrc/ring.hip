@@ -4,6 +4,10 @@
 // reduction op, compiled in parallel).
 #include "ring_kernel.h"
 
+namespace mccs {
+int comm_fifo_slots_of(const void* d_comm);  // host/comm.cpp
+}
+
 #include <mutex>
 #include <vector>
 
@@ -129,6 +133,10 @@ extern "C" mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, mccsDe
   // blocks of one wave have no control wave (ring_kernel.h); the reference
   // host never launches fewer than 96 threads (get_task_schema, plan.rs:602-635)
   if (!fn || !comm || !workHead || grid == 0 || block <= 64 || block > MCCS_RING_MAX_THREADS) return mccsInvalidArgument;
+  // a communicator of this library with a deeper FIFO ring: the kernels below
+  // index the reference's 8 slots (kRefCfg), its peers' launches would not
+  const int fs = mccs::comm_fifo_slots_of(comm);
+  if (fs != 0 && fs != MCCS_BUFFER_SLOTS) return mccsInvalidUsage;
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return mccsUnhandledCudaError;
   std::lock_guard<std::mutex> lk(g_ext_mu);

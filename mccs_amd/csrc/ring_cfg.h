@@ -28,6 +28,12 @@
 // always run with the reference defaults (system-scope fences, 2-step slices).
 #define MCCS_FENCE_SYSTEM 0   // FIFO memory may be cached: system-scope release/acquire
 #define MCCS_FENCE_UNCACHED 1 // FIFO memory is uncached (hipDeviceMallocUncached): drains only
+// Uncached FIFO memory, but a system-scope release fence before every post
+// (the analogue of __threadfence_system before postPeer, prims_simple.h:
+// 120-125,211); polls stay relaxed.  The step between relaxed hand-offs and
+// the cached-memory mode for links where a drained store might not yet be
+// visible to the peer when the flag lands.
+#define MCCS_FENCE_UNCACHED_RELEASE 2
 
 // Error bits a ring kernel reports for ONE communicator: word 1 of the
 // communicator's own abort line (abortFlag[1]; the library allocates that line,

@@ -114,9 +114,14 @@ MAX_RING_WORKGROUPS = 256
 
 
 def _candidates(C, lanes_opts, locs, chan_opts=(None,)):
-    """Transport candidates in preference order; within one (placement,
-    channels, lanes) the cached-FIFO arena is used only if the uncached one
-    cannot be created or exported."""
+    """Transport candidates in preference order.  Within one (placement,
+    channels, lanes) the hand-off modes go from cheapest to safest, each tried
+    only when the one before it cannot be created or fails the exact-sum gate:
+      1. uncached FIFO arena, relaxed hand-offs (drain, then post);
+      2. uncached FIFO arena + a system-scope release fence before every post
+         (the reference's __threadfence_system before postPeer,
+         prims_simple.h:120-125,211);
+      3. cached (hipMalloc) arena + system-scope release/acquire."""
     out = []
     for loc in locs:
         lname = {None: "env", C.LOCALITY_RECEIVER: "receiver", C.LOCALITY_SENDER: "sender"}[loc]
@@ -128,7 +133,9 @@ def _candidates(C, lanes_opts, locs, chan_opts=(None,)):
                 if nch:
                     kw["channel_count"] = nch
                 tag = f"{lname}/lanes={lanes or 'auto'}" + (f"/channels={nch}" if nch else "")
-                out.append((tag, [(f"{lname}-uncached-fifo", C.CommConfig(**kw)),
+                out.append((tag, [(f"{lname}-uncached-fifo", C.CommConfig(fifo_memory=C.FIFO_UNCACHED, **kw)),
+                                  (f"{lname}-uncached-fifo+release-fence",
+                                   C.CommConfig(fifo_memory=C.FIFO_UNCACHED_RELEASE, **kw)),
                                   (f"{lname}-cached-fifo+system-fences",
                                    C.CommConfig(fifo_memory=C.FIFO_DEVICE, **kw))]))
     return out

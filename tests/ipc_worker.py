@@ -45,13 +45,15 @@ def main():
     # sender-side: remote reads, the reference SHM layout)
     all_modes = {"uncached": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER), "device": (C.FIFO_DEVICE, C.LOCALITY_RECEIVER),
                  "sender-uncached": (C.FIFO_UNCACHED, C.LOCALITY_SENDER),
-                 "sender-device": (C.FIFO_DEVICE, C.LOCALITY_SENDER)}
+                 "sender-device": (C.FIFO_DEVICE, C.LOCALITY_SENDER),
+                 "release": (C.FIFO_UNCACHED_RELEASE, C.LOCALITY_RECEIVER),
+                 "sender-release": (C.FIFO_UNCACHED_RELEASE, C.LOCALITY_SENDER)}
     names = os.environ.get("IPC_MODES", "uncached,device").split(",")
     results = {}
-    # two processes on one GPU: their kernels must be co-resident, so keep the
-    # pair at 128 workgroups (4 channels x 16 lanes, ring_bench.shared_gpu_lanes)
-    # rather than the node default of 128 per rank
-    lanes = 16 if world == 2 and torch.cuda.device_count() < world else None
+    # processes sharing one GPU: the library's default lanes; mccsCommConnect
+    # shrinks them so every rank's workgroups fit in half the GPU's ring slots
+    # (2 ranks x 4 channels x 16 lanes = 128 of 256)
+    lanes = None
     for mode in names:
         fifo, loc = all_modes[mode]
         comm = C.init_communicator_rank(rank, world, dev, exchange,
@@ -84,6 +86,11 @@ def main():
                 print(f"[rank {rank}] {mode} code={code}: {e}", flush=True)
                 ok = False
             results[f"{mode}/dtype{code}/n{count}"] = ok
+        if torch.cuda.device_count() < world:  # co-located processes: lanes shrunk to half the ring slots
+            # auto lanes (api.cpp make_comm) capped at half of MI355X's 256 one-per-CU ring slots
+            auto = (128 if world == 2 else 64) // comm.nchannels
+            want = min(auto, 256 // 2 // (world * comm.nchannels))
+            results[f"{mode}/colocated_lanes={comm.lanes}"] = comm.lanes == want
         comm.destroy()
     allres = [None] * world
     dist.all_gather_object(allres, results)

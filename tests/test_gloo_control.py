@@ -168,8 +168,13 @@ def _gate_worker(rank, world, port, q):
         c2, n2 = rb.make_validated_comm(None, dist, fc, rank, world, 0, None, ex, m2, None, rejected=rej, gate=gate)
         c3, n3 = rb.make_validated_comm(None, dist, fc, rank, world, 0, None, ex, m1, None, rejected=[],
                                         gate=lambda c: False)
+        # three hand-off modes: relaxed fails on rank 1 only, the release-fence mode passes
+        m4 = [("receiver-uncached-fifo", "U"), ("receiver-uncached-fifo+release-fence", "R"),
+              ("receiver-cached-fifo+system-fences", "D")]
+        rej4 = []
+        c4, n4 = rb.make_validated_comm(None, dist, fc, rank, world, 0, None, ex, m4, None, rejected=rej4, gate=gate)
         q.put((rank, n1, n2, n3, [r["kind"] for r in rej], len(fc.made), fc.made[0].destroyed,
-               c1.destroyed, c2.destroyed))
+               c1.destroyed, c2.destroyed, n4, [r["kind"] for r in rej4]))
     finally:
         dist.destroy_process_group()
 
@@ -191,9 +196,11 @@ def test_bench_gate_rejects_a_mode_on_every_rank_and_records_it():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, n1, n2, n3, kinds, made, first_destroyed, c1_destroyed, c2_destroyed in res:
+    for rank, n1, n2, n3, kinds, made, first_destroyed, c1_destroyed, c2_destroyed, n4, kinds4 in res:
+        assert n4 == "receiver-uncached-fifo+release-fence" and kinds4 == ["uncached-fifo"]
         assert n1 == "receiver-cached-fifo+system-fences" and n2 == "sender-cached-fifo+system-fences"
         assert n3 is None
         assert kinds == ["uncached-fifo"]
-        # m1: U (rejected, destroyed) + D; m2: U skipped, D; m1 again with a fresh list: U + D both rejected
-        assert made == 5 and first_destroyed and not c1_destroyed and not c2_destroyed
+        # m1: U (rejected, destroyed) + D; m2: U skipped, D; m1 again with a fresh list: U + D both
+        # rejected; m4: U (rejected) + R
+        assert made == 7 and first_destroyed and not c1_destroyed and not c2_destroyed

@@ -40,7 +40,7 @@ def test_colocated_external_launch_refused_while_peer_runs():
     f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                   ctypes.c_uint, ctypes.c_uint, ctypes.c_void_p]
     f.restype = ctypes.c_int
-    comms = C.init_all([0, 0], C.CommConfig(lanes=1, timeout_ms=20000))
+    comms = C.init_all([0, 0], C.CommConfig(lanes=1, timeout_ms=20000, fifo_slots=8))
     try:
         nch, nthr, count = comms[0].nchannels, 544, 1 << 20
         xs = [torch.ones(count, device="cuda") for _ in range(2)]
@@ -78,3 +78,26 @@ def test_colocated_external_launch_refused_while_peer_runs():
         assert all(np.all(o == 2.0) for o in outs)
     finally:
         vnode.destroy(fresh)
+
+
+def test_external_launch_refuses_a_deeper_fifo_communicator():
+    """The reference-named kernels index the reference's 8 FIFO slots; a
+    library communicator built with 16 (the default) is refused before
+    anything is launched (its peers would index another slot ring)."""
+    import torch
+
+    lib = _lib.load()
+    comms = C.init_all([0, 0], C.CommConfig(lanes=1))
+    try:
+        nch, nthr, count = comms[0].nchannels, 544, 1 << 10
+        x, y = torch.ones(count, device="cuda"), torch.zeros(count, device="cuda")
+        wb = torch.frombuffer(bytearray(bytes(_works(nch, x.data_ptr(), y.data_ptr(), count, nthr))),
+                              dtype=torch.uint8).cuda()
+        rc = lib.mccs_hip_launch_coll(FUNC_ALLREDUCE, F32, 0, comms[0].dev_comm(), (1 << nch) - 1, wb.data_ptr(), nch,
+                                      nthr, torch.cuda.current_stream().cuda_stream)
+        assert rc == INVALID_USAGE, rc
+        torch.cuda.synchronize()
+        assert torch.all(y == 0)
+    finally:
+        for c in comms:
+            c.destroy()

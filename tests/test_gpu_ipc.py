@@ -24,7 +24,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,modes", [(2, "uncached,device,sender-uncached,sender-device"),
+@pytest.mark.parametrize("world,modes", [(2, "uncached,device,sender-uncached,sender-device,release,sender-release"),
                                          (4, "uncached,sender-uncached")])
 def test_multi_process_ring_matches_oracle(world, modes):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",

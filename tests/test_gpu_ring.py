@@ -213,6 +213,8 @@ CONFIGS = [
     dict(locality=C.LOCALITY_SENDER),
     dict(locality=C.LOCALITY_SENDER, lanes=2),
     dict(fifo_memory=C.FIFO_DEVICE),
+    dict(fifo_memory=C.FIFO_UNCACHED_RELEASE),  # release fence before every post
+    dict(fifo_memory=C.FIFO_UNCACHED_RELEASE, locality=C.LOCALITY_SENDER, fifo_slots=8),
     dict(buffer_size=1 << 20),
     dict(channel_count=2, rings="default", block_threads=544, lanes=1),  # reference profile
     dict(channel_count=5),

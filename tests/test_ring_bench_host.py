@@ -92,6 +92,20 @@ def test_channel_options_double_the_rings_on_distinct_gpus(monkeypatch):
     assert rb.channel_options(C, 8, False) == [None]
 
 
+def test_handoff_modes_go_from_relaxed_to_release_fence_to_cached():
+    """Gate order within every candidate: relaxed uncached hand-offs, then the
+    uncached arena with a release fence before each post, then the cached
+    arena with system-scope fences; each is a distinct rejectable kind."""
+    for tag, modes in rb._candidates(C, [None], [C.LOCALITY_RECEIVER, C.LOCALITY_SENDER]):
+        names = [n for n, _ in modes]
+        loc = tag.split("/")[0]
+        assert names == [f"{loc}-uncached-fifo", f"{loc}-uncached-fifo+release-fence",
+                         f"{loc}-cached-fifo+system-fences"]
+        assert [cfg.fifo_memory for _, cfg in modes] == [C.FIFO_UNCACHED, C.FIFO_UNCACHED_RELEASE, C.FIFO_DEVICE]
+        kinds = [n.split("-", 1)[-1] for n in names]
+        assert len(set(kinds)) == 3
+
+
 def test_candidates_stay_within_coresident_workgroups():
     cands = rb._candidates(C, [None, 16, 32], [C.LOCALITY_RECEIVER], [None, 14])
     tags = [t for t, _ in cands]
