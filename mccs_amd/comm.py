@@ -121,6 +121,11 @@ class Communicator:
 
     def __init__(self, handle: int):
         self._h = ctypes.c_void_p(handle)
+        self._load_info()
+
+    def _load_info(self) -> None:
+        """(Re)reads the comm's profile; mccsCommConnect may shrink the lanes of
+        co-located processes and settle the hand-off mode."""
         info = (_ci * 7)()
         _lib.check(_sig().mccsCommInfo(self._h, info), "mccsCommInfo")
         (self.rank, self.nranks, self.device, self.nchannels, self.lanes, self.block_threads,
@@ -201,6 +206,7 @@ def init_communicator_rank(rank: int, nranks: int, device: int, exchange, config
     if rc != 0:
         comm.destroy()
         _lib.check(rc, "mccsCommConnect")
+    comm._load_info()
     return comm
 
 
