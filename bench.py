@@ -112,6 +112,47 @@ def cpu_baseline(dtype_code: int, nelem: int, budget_s: float) -> dict:
     }
 
 
+def ring_cpu_baseline(world: int, nbytes: int, dtype_code: int = 7, budget_s: float = 6.0) -> dict:
+    """N > 1 lines: the host computes the AllReduce result itself -- the
+    elementwise sum of `world` buckets of `nbytes` (oracle_reduce_mt, C,
+    pthreads) on every hardware thread this process may use, plus one
+    thread.  value = S / t, comparable with algbw; the host moved (n+1)*S
+    bytes per pass.  A bucket larger than 256 MiB is sampled (its first
+    256 MiB), so the leg stays within budget_s."""
+    import numpy as np
+
+    from mccs_amd import ring_bench as rb
+    from oracle import oracle as orc
+
+    npdt = orc.NP_DTYPE[dtype_code]
+    esz = np.dtype(npdt).itemsize
+    sample = min(nbytes, 256 << 20)
+    n = sample // esz
+    rng = np.random.default_rng(0x6D636373)
+    srcs = [(rng.random(n, dtype=np.float32) * 2 - 1).astype(npdt) for _ in range(world)]
+    dst = np.empty_like(srcs[0])
+    threads = cpu_threads()
+    res = {}
+    for label, nthr, share in (("mt", threads, 0.8), ("st", 1, 0.2)):
+        orc.reduce_mt(dtype_code, orc.SUM, srcs, dst, nthr)  # page in
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            orc.reduce_mt(dtype_code, orc.SUM, srcs, dst, nthr)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s * share or (label == "st" and reps >= 1):
+                break
+        res[label] = (sample * reps / el / 1e9, nthr, reps, el)
+    gbps, nthr, reps, el = res["mt"]
+    tname = {6: "fp16", 7: "fp32", 9: "bf16"}.get(dtype_code, str(dtype_code))
+    return {"value": round(gbps, 3), "unit": "GB/s of bucket (S/t, as algbw)", "cores": nthr, "kind": "port",
+            "sample": f"{world} x {sample >> 20} MiB {tname} -> 1 sum (oracle_reduce_mt)"
+                      + (f", first {sample >> 20} MiB of the {nbytes >> 20} MiB bucket" if sample < nbytes else "")
+                      + f", {reps} passes in {el:.2f}s on {nthr} threads = {gbps * (world + 1):.1f} GB/s of host "
+                        f"memory traffic; 1-thread {res['st'][0]:.3f} GB/s",
+            "single_thread_value": round(res["st"][0], 3), "host": rb.host_record()}
+
+
 def host_loopback_latency(calls: int = 200) -> dict:
     """BASELINE configs[0]: 2-rank loopback AllReduce of 1 KiB fp32 on host
     threads (mccs_host_ring_allreduce: the ring protocol over host memory,
@@ -378,7 +419,7 @@ def main():
     if world > 1 or args.gpus > 1:
         from mccs_amd import ring_bench
 
-        out = ring_bench.run(args)
+        out = ring_bench.run(args, cpu_sum_baseline=ring_cpu_baseline)
         if out is None:  # non-zero rank
             return
     else:

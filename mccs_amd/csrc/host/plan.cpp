@@ -248,6 +248,15 @@ static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
     c->work_next = first;
   }
   MCCS_CHECK(wait_work_queue(c, first + work_count));
+  // Acknowledgements: a chained channel's last work sits at `subsequent`, so
+  // subsequent + 1 (plan.rs:461-470) is one past it.  A single-work channel's
+  // entry is first + nth, where plan.rs's subsequent + 1 = first + nchan + 1
+  // reaches one entry PAST this launch: once read, it would release the
+  // next launch's first entry before that launch has read it.  Here a
+  // single work acknowledges the launch's end; entries of this launch not
+  // yet read by other channels stay covered by wait_work_queue's minimum
+  // over busy channels.
+  const uint32_t launch_end = first + work_count;
   uint32_t subsequent = first + nchan;
   for (uint32_t nth = 0; nth < nchan; ++nth) {
     const int ch = chan_list[nth];
@@ -255,8 +264,9 @@ static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
     for (size_t wid = 0; wid < works.size(); ++wid) {
       mccsDevWork dw;
       if (wid == works.size() - 1) {
-        c->chan_next[ch] = subsequent + 1;
-        dw = to_dev_work(works[wid], true, true, subsequent + 1);
+        const uint32_t ack = works.size() == 1 ? launch_end : subsequent + 1;
+        c->chan_next[ch] = ack;
+        dw = to_dev_work(works[wid], true, true, ack);
       } else {
         const uint32_t nxt = (wid == 0 ? subsequent : subsequent + 1) & qmask;
         dw = to_dev_work(works[wid], false, false, (uint32_t)((int32_t)nxt - (int32_t)(first & qmask)));

@@ -1,0 +1,206 @@
+"""In-process multi-device legs of the N > 1 bench line (rank 0, ranks 1..N-1
+parked at a barrier).
+
+* in_process_multi_device: the reference's own service model -- ONE process
+  drives every GPU of the node (src/mccs/src/control.rs:244-282; the SHM
+  connector is an in-process pointer, transport/shm/transporter.rs:76-78):
+  mccsCommInitAll over devices 0..N-1 (peer access between every pair), one
+  grouped AllReduce = one launch per device, exact-sum gated, algbw at the
+  bucket size of the line.
+* xgmi_calibration: what the links give this library's own copy kernel
+  (mccs_hip_reduce_copy, 1 source -> 1 destination, the register streaming
+  loop) when one side of the copy is a peer GPU's HBM: one link alone in
+  each direction (pull = read the peer, push = write the peer), both
+  directions of one link at once, every link of device 0 at once, and the
+  ring's load -- every device pushing to every peer at once.  The ring's
+  roofline is then priced against the measured per-direction rate beside
+  the spec figure.
+
+Both run only when this process sees at least `world` GPUs; on a box whose
+ranks share one GPU they report "n/a".  Every exception is caught and
+recorded: these legs never fail the line.
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+
+
+def _hip():
+    from .refdrive import hip
+
+    h = hip()
+    h.hipDeviceCanAccessPeer.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int]
+    h.hipDeviceEnablePeerAccess.argtypes = [ctypes.c_int, ctypes.c_uint]
+    return h
+
+
+def enable_peer_access(torch, devices) -> None:
+    """hipDeviceEnablePeerAccess between every ordered pair of distinct devices
+    (already-enabled is fine)."""
+    h = _hip()
+    for a in devices:
+        for b in devices:
+            if a == b:
+                continue
+            can = ctypes.c_int(0)
+            if h.hipDeviceCanAccessPeer(ctypes.byref(can), a, b) != 0 or not can.value:
+                raise RuntimeError(f"device {a} cannot access device {b}")
+            with torch.cuda.device(a):
+                rc = h.hipDeviceEnablePeerAccess(b, 0)
+            if rc not in (0, 704):  # 704 = hipErrorPeerAccessAlreadyEnabled
+                raise RuntimeError(f"hipDeviceEnablePeerAccess({a} -> {b}) = {rc}")
+    h.hipGetLastError()
+
+
+def _exact(torch, n, rank, dev):
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    return ((i * 7 + rank * 13) % 511) - 255  # k/64, |k| <= 255: exact sums for <= 8 ranks
+
+
+def in_process_multi_device(torch, C, world: int, nbytes: int, warmup: int = 3, steps: int = 10,
+                            devices=None) -> dict:
+    """One process, `world` ranks on `devices` (default 0..world-1): exact-sum
+    gate, then `steps` grouped AllReduces of nbytes fp32 per rank."""
+    devices = list(devices if devices is not None else range(world))
+    n = nbytes // 4
+    comms = C.init_all(devices)
+    try:
+        xs, ys, sts = [], [], []
+        for r, d in enumerate(devices):
+            dev = torch.device("cuda", d)
+            xs.append((_exact(torch, n, r, dev).to(torch.float32) / 64.0))
+            ys.append(torch.empty_like(xs[-1]))
+            sts.append(torch.cuda.Stream(device=dev))
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+
+        def step():
+            with C.group():
+                for r in range(world):
+                    C.all_reduce(comms[r], xs[r], ys[r], n, C.AllReduceDataType.Float32, C.AllReduceOpType.Sum,
+                                 stream=sts[r])
+
+        def sync_all():
+            for s in sts:
+                s.synchronize()
+            for c in comms:
+                c.sync()
+
+        step()
+        sync_all()
+        ok = True
+        for r, d in enumerate(devices):
+            dev = torch.device("cuda", d)
+            tot = torch.zeros(n, dtype=torch.int64, device=dev)
+            for q in range(world):
+                tot += _exact(torch, n, q, dev)
+            ok = ok and bool(torch.equal(ys[r], (tot.to(torch.float64) / 64.0).to(torch.float32)))
+            del tot
+        res = {"devices": devices, "channels": comms[0].nchannels, "lanes": comms[0].lanes,
+               "exact_sum_full_size": ok}
+        if not ok:
+            return res
+        for _ in range(warmup):
+            step()
+        sync_all()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        sync_all()
+        per = (time.perf_counter() - t0) / steps
+        res.update(ms_per_allreduce=round(per * 1e3, 4), algbw_GBps=round(nbytes / per / 1e9, 3),
+                   busbw_GBps=round(nbytes / per / 1e9 * 2 * (world - 1) / world, 3), steps=steps)
+        return res
+    finally:
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+        for c in comms:
+            c.destroy()
+
+
+def xgmi_calibration(torch, devices, nbytes: int = 64 << 20, reps: int = 10) -> dict:
+    """Copy bandwidth (GB/s of bytes copied, wall time over `reps` launches
+    per stream after a warm-up) with one side of the copy on a peer GPU.
+    `devices[0]` is the local GPU.  Uses mccs_hip_reduce_copy with the
+    register streaming loop (the access pattern of the ring's reduce-copy)."""
+    from . import reduce as R
+
+    devices = list(devices)
+    nd = len(devices)
+    distinct = len(set(devices)) == nd
+    if distinct:
+        enable_peer_access(torch, devices)
+    n = nbytes // 4
+    bufs = {}
+
+    def buf(i, tag):
+        """A buffer in the HBM of devices[i] (indices, so a one-GPU smoke run
+        with repeated devices exercises the same code)."""
+        if (i, tag) not in bufs:
+            bufs[(i, tag)] = torch.empty(n, dtype=torch.float32, device=torch.device("cuda", devices[i])).fill_(1.0)
+        return bufs[(i, tag)]
+
+    saved = R.get_tune()
+
+    def timed(jobs):
+        """jobs: list of (launching device index, dst tensor, src tensor); each
+        on its own stream of its launching device, all concurrently."""
+        streams = [torch.cuda.Stream(device=torch.device("cuda", devices[i])) for i, _, _ in jobs]
+
+        def run(k):
+            for (i, dst, src), st in zip(jobs, streams):
+                with torch.cuda.device(devices[i]):
+                    for _ in range(k):
+                        R.reduce_copy([dst], [src], count=n, stream=st)
+        run(1)
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+        t0 = time.perf_counter()
+        run(reps)
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+        el = time.perf_counter() - t0
+        return len(jobs) * reps * nbytes / el / 1e9
+
+    out = {"bytes_per_copy": nbytes, "reps": reps, "kernel": "mccs_hip_reduce_copy 1->1 (REG loop, nt)",
+           "peers_distinct_gpus": distinct}
+    try:
+        peers = range(1, nd)
+        # one link alone: full-grid copies
+        R.tune(1, 4, 1, 4, 0, 0)
+        out["one_link"] = {
+            "peer": devices[1],
+            "pull_GBps": round(timed([(0, buf(0, "dst"), buf(1, "src"))]), 2),
+            "push_GBps": round(timed([(0, buf(1, "dst"), buf(0, "src"))]), 2),
+        }
+        # both directions of that link at once (each side pushes)
+        R.tune(1, 4, 1, 2, 0, 0)
+        bi = timed([(0, buf(1, "dst"), buf(0, "src")), (1, buf(0, "dst"), buf(1, "src"))])
+        out["one_link"]["bidirectional_push_GBps_total"] = round(bi, 2)
+        # every peer of device 0 alone, push and pull (link uniformity)
+        R.tune(1, 4, 1, 4, 0, 0)
+        out["per_peer"] = [{"peer": devices[q], "pull_GBps": round(timed([(0, buf(0, "dst"), buf(q, "src"))]), 2),
+                            "push_GBps": round(timed([(0, buf(q, "dst"), buf(0, "src"))]), 2)} for q in peers]
+        # every link of device 0 at once (one stream per peer, 1 block per CU each)
+        R.tune(1, 4, 1, 1, 0, 0)
+        out["all_links_of_dev0"] = {
+            "pull_GBps_total": round(timed([(0, buf(0, f"dst{q}"), buf(q, "src")) for q in peers]), 2),
+            "push_GBps_total": round(timed([(0, buf(q, "dst0"), buf(0, "src")) for q in peers]), 2),
+        }
+        # the ring's load: every device pushes to every peer at once
+        jobs = [(a, buf(b, f"dst{a}"), buf(a, "src")) for a in range(nd) for b in range(nd) if a != b]
+        tot = timed(jobs)
+        out["all_to_all_push"] = {"GBps_total": round(tot, 2), "directed_links": len(jobs),
+                                  "GBps_per_link_direction": round(tot / len(jobs), 2)}
+        out["per_link_direction_GBps"] = out["all_to_all_push"]["GBps_per_link_direction"]
+    except Exception as e:  # recorded, never fatal
+        out["error"] = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        R.tune(saved["variant"], saved["unroll"], saved["policy"], saved["blocks_per_cu"], saved["stages"],
+               saved["waves"])
+        bufs.clear()
+        for d in set(devices):
+            torch.cuda.synchronize(d)
+        torch.cuda.empty_cache()
+    return out

@@ -81,6 +81,69 @@ def reference_rings(n: int, nch: int) -> list[list[int]]:
     return [list(range(n)) for _ in range(nch)]
 
 
+class WorkRing:
+    """plan.rs's work-FIFO bookkeeping (upload_work's slot reservation,
+    wait_work_queue's rolling acknowledgements, plan.rs:380-541), host-only so
+    it is unit-tested on CPU.  One work per selected channel per launch.
+
+    Acknowledgement value: plan.rs:461-470 gives a channel's single (first
+    and last) work DoneAcks(new_subsequent_start + 1) = first + k + 1, one
+    entry PAST the launch's last entry.  Once that launch is read, the
+    host's acked_min therefore also covers the first entry of the NEXT
+    launch, which may not have been read yet: a host a full ring ahead can
+    overwrite it (tests/test_refdrive_host.py reproduces the overwrite).
+    By default the acknowledgement here is the launch's end, first + k
+    (exact; NCCL's doneAcks is likewise one past the channel's last work);
+    `reference_acks=True` keeps the reference arithmetic."""
+
+    def __init__(self, nch: int, depth: int = WORK_DEPTH, reference_acks: bool = False):
+        assert depth & (depth - 1) == 0
+        self.nch, self.depth = nch, depth
+        self.reference_acks = reference_acks
+        self.next_available = 0
+        self.chan_next = [0] * nch
+        self.acked_min = 0
+
+    def _wait(self, target: int, read_done, write_done, timeout_s: float) -> None:
+        """plan.rs:380-422."""
+        if not _rolling_less((self.acked_min + self.depth) & 0xFFFFFFFF, target & 0xFFFFFFFF):
+            return
+        t0 = time.monotonic()
+        while True:
+            ackd = read_done()
+            ackd_all = self.next_available
+            for c in range(self.nch):
+                if ackd[c] != self.chan_next[c]:
+                    ackd_all = _rolling_min(ackd_all, ackd[c])
+            for c in range(self.nch):
+                if ackd[c] == self.chan_next[c]:
+                    write_done(c, ackd_all)
+            self.acked_min = ackd_all
+            if not _rolling_less((self.acked_min + self.depth) & 0xFFFFFFFF, target & 0xFFFFFFFF):
+                return
+            if time.monotonic() - t0 > timeout_s:
+                raise RuntimeError("reference-driven work ring: no acknowledgement (kernel stuck?)")
+            time.sleep(0)
+
+    def reserve(self, chans, read_done, write_done, timeout_s: float = 60.0):
+        """Slots for one launch over `chans` (ascending channel ids): returns
+        (first slot counter, doneAcks).  Wraps to the ring start rather than
+        splitting a launch's works, and waits until the slots are acknowledged
+        (upload_work, plan.rs:424-443)."""
+        k = len(chans)
+        mask = self.depth - 1
+        start = self.next_available
+        if ((start + k - 1) & mask) < (start & mask):
+            start = (start + mask) & ~mask & 0xFFFFFFFF
+            self.next_available = start
+        self._wait(start + k, read_done, write_done, timeout_s)
+        acks = (start + k + (1 if self.reference_acks else 0)) & 0xFFFFFFFF
+        for c in chans:
+            self.chan_next[c] = acks
+        self.next_available = (start + k) & 0xFFFFFFFF
+        return start, acks
+
+
 class RefDrivenRank:
     """One rank's device structures, built as the Rust service builds them.
 
@@ -155,9 +218,7 @@ class RefDrivenRank:
         self.d_comm = self._upload(bytes(hc))
         # -- planner state (plan.rs)
         self.load = [0] * nch
-        self.next_available = 0
-        self.chan_next = [0] * nch
-        self.acked_min = 0
+        self.ring = WorkRing(nch)
         self.launches = 0
         self._works = {}
 
@@ -191,27 +252,11 @@ class RefDrivenRank:
         return p
 
     # plan.rs ---------------------------------------------------------------
-    def _wait_work_queue(self, target: int, timeout_s: float = 60.0) -> None:
-        """plan.rs:380-422."""
-        if not _rolling_less((self.acked_min + WORK_DEPTH) & 0xFFFFFFFF, target & 0xFFFFFFFF):
-            return
-        done = (ctypes.c_uint32 * abi.MCCS_MAX_NCHANNELS).from_address(self.h_done)
-        t0 = time.monotonic()
-        while True:
-            ackd = list(done)
-            ackd_all = self.next_available
-            for c in range(self.nch):
-                if ackd[c] != self.chan_next[c]:
-                    ackd_all = _rolling_min(ackd_all, ackd[c])
-            for c in range(self.nch):
-                if ackd[c] == self.chan_next[c]:
-                    done[c] = ackd_all
-            self.acked_min = ackd_all
-            if not _rolling_less((self.acked_min + WORK_DEPTH) & 0xFFFFFFFF, target & 0xFFFFFFFF):
-                return
-            if time.monotonic() - t0 > timeout_s:
-                raise RuntimeError("reference-driven work ring: no acknowledgement (kernel stuck?)")
-            time.sleep(0)
+    def _read_done(self):
+        return list((ctypes.c_uint32 * abi.MCCS_MAX_NCHANNELS).from_address(self.h_done))
+
+    def _write_done(self, c, v):
+        (ctypes.c_uint32 * abi.MCCS_MAX_NCHANNELS).from_address(self.h_done)[c] = v
 
     def all_reduce(self, send_ptr: int, recv_ptr: int, count: int, dtype: int, op: int, stream: int) -> None:
         """One AllReduce task through plan.rs's path (one work element per
@@ -226,12 +271,7 @@ class RefDrivenRank:
         for c in chans:
             self.load[c] += nbytes
         mask_q = WORK_DEPTH - 1
-        start = self.next_available
-        if ((start + k - 1) & mask_q) < (start & mask_q):  # wrap to the ring start
-            start = (start + mask_q) & ~mask_q & 0xFFFFFFFF
-            self.next_available = start
-        self._wait_work_queue(start + k)
-        acks = (start + k + 1) & 0xFFFFFFFF
+        start, acks = self.ring.reserve(chans, self._read_done, self._write_done)
         key = (send_ptr, recv_ptr, count, k, nthr)
         works = self._works.get(key)
         if works is None:  # work_elem_conversion (plan.rs:550-600), built once per shape
@@ -248,13 +288,11 @@ class RefDrivenRank:
             if len(self._works) > 64:
                 self._works.clear()
             self._works[key] = works
-        for nth, c in enumerate(chans):
+        for nth in range(k):
             w = works[nth]
             w.header.doneAcks = acks
             ctypes.memmove(self.h_work + ((start + nth) & mask_q) * abi.MCCS_WORK_SIZE, ctypes.addressof(w),
                            abi.MCCS_WORK_SIZE)
-            self.chan_next[c] = acks
-        self.next_available = (start + k) & 0xFFFFFFFF
         channel_mask = 0
         for c in chans:
             channel_mask |= 1 << c

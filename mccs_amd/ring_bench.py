@@ -402,39 +402,6 @@ def host_record() -> dict:
     return rec
 
 
-def cpu_sum_baseline(world: int, nbytes: int, budget_s: float = 6.0) -> dict:
-    """Host elementwise sum of `world` buffers of `nbytes` fp32 each (the
-    AllReduce result computed by the host) on every hardware thread this
-    process may use, same bucket size as the timed ring.  value = S / t,
-    comparable with algbw; the bytes the host moved per pass are (n+1)*S."""
-    import numpy as np
-
-    from oracle import oracle as orc
-
-    n = nbytes // 4
-    rng = np.random.default_rng(0x6D636373)
-    srcs = [rng.random(n, dtype=np.float32) * 2 - 1 for _ in range(world)]
-    dst = np.empty_like(srcs[0])
-    threads = len(os.sched_getaffinity(0))
-    res = {}
-    for label, nthr, share in (("mt", threads, 0.8), ("st", 1, 0.2)):
-        orc.reduce_mt(7, orc.SUM, srcs, dst, nthr)  # page in
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            orc.reduce_mt(7, orc.SUM, srcs, dst, nthr)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= budget_s * share or (label == "st" and reps >= 1):
-                break
-        res[label] = (nbytes * reps / el / 1e9, nthr, reps, el)
-    gbps, nthr, reps, el = res["mt"]
-    return {"value": round(gbps, 3), "unit": "GB/s of bucket (S/t, as algbw)", "cores": nthr, "kind": "port",
-            "sample": f"full workload: {world} x {nbytes >> 20} MiB fp32 -> 1 sum (oracle_reduce_mt), {reps} passes "
-                      f"in {el:.2f}s on {nthr} threads = {gbps * (world + 1):.1f} GB/s of host memory traffic; "
-                      f"1-thread {res['st'][0]:.3f} GB/s",
-            "single_thread_value": round(res["st"][0], 3), "host": host_record()}
-
-
 def cpu_ring_baseline(world: int, nbytes: int, nchannels: int, budget_s: float = 4.0) -> dict:
     """SURVEY §8(d) configs[2]: the same ring schedule run by host threads
     over host memory (mccs_host_ring_allreduce: `world` ranks x `nchannels`
@@ -483,7 +450,7 @@ def ring_roofline(world, nbytes, per_step_s, links, ranks_share_gpu, kernel):
 
 
 def ring_line(*, world, steps, warmup, per_step_s, nbytes, dt_name, comm_info, rings, mode, tune_table, prof,
-              ranks_share_gpu, cpu_baseline, extras=None) -> dict:
+              ranks_share_gpu, cpu_baseline, extras=None, calibration=None) -> dict:
     """The N > 1 bench line (pure: no GPU, unit-tested on CPU)."""
     algbw = nbytes / per_step_s / 1e9
     line = {
@@ -519,10 +486,22 @@ def ring_line(*, world, steps, warmup, per_step_s, nbytes, dt_name, comm_info, r
     for k, v in (extras or {}).items():
         if v is not None:
             line["config"][k] = v
+    per_dir = (calibration or {}).get("per_link_direction_GBps")
+    rf = line["roofline"]
+    if rf["bound"] == "xgmi" and per_dir:
+        # the same links priced at the rate this node's copy kernel measured
+        # with every device pushing to every peer at once (node_probe)
+        links = out_links(rings, 0)
+        rf["peak_calibrated"] = round(links * per_dir, 2)
+        rf["frac_calibrated"] = round(rf["achieved"] / rf["peak_calibrated"], 4)
+        rf["calibration"] = f"{links} links x {per_dir} GB/s per direction (all-to-all push, measured this run)"
     return line
 
 
-def run(args):
+def run(args, cpu_sum_baseline=None):
+    """`cpu_sum_baseline(world, nbytes, dtype_code) -> dict`: the host-CPU
+    baseline leg, supplied by bench.py (it times the oracle's threaded C sum,
+    which the product package never imports)."""
     import torch
     import torch.distributed as dist
 
@@ -543,14 +522,14 @@ def run(args):
     try:
         if getattr(args, "jobs", None) in ("setup2", "setup2-interleaved"):
             return run_setup2(args, torch, dist, C, rank, world, device, dev,
-                              interleaved=args.jobs.endswith("interleaved"))
-        return _run_ring(args, torch, dist, C, rank, world, device, dev, ndev)
+                              interleaved=args.jobs.endswith("interleaved"), cpu_sum_baseline=cpu_sum_baseline)
+        return _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_baseline)
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
 
 
-def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
+def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_baseline=None):
     exchange = _exchange_factory(dist, world)
     dt_name = args.dtype
     tdt = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[dt_name]
@@ -613,12 +592,21 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
         extras["configs4_two_jobs"] = setup2_measure(torch, dist, C, rank, world, device, dev, False,
                                                      warmup=1, iters=int(os.environ.get("MCCS_SETUP2_ITERS", "10")))
     dist.barrier()
+    if not getattr(args, "no_extra", False) and os.environ.get("MCCS_BENCH_NO_REFDRV") != "1":
+        extras["reference_driven"] = reference_driven_leg(torch, dist, rank, world, device, nbytes)
+    calib = None
+    if not getattr(args, "no_extra", False):
+        # rank 0 alone drives every GPU; ranks 1..N-1 wait at the barrier below
+        if rank == 0:
+            extras["in_process_multi_device"], calib = node_legs(torch, C, world, ndev, nbytes)
+            extras["xgmi_calibration"] = calib
+        dist.barrier()
     if rank != 0:
         dist.barrier()  # rank 0 times the host baseline
         return None
     cpu = None
-    if not getattr(args, "no_cpu_baseline", False):
-        cpu = cpu_sum_baseline(world, nbytes)
+    if not getattr(args, "no_cpu_baseline", False) and cpu_sum_baseline is not None:
+        cpu = cpu_sum_baseline(world, nbytes, 7)
         # host threads = world x channels: at most the default channel count
         # (a doubled-channel transport would double the spinning threads)
         host_ch = min(info["channels"], len(C.default_rings(world, 0)))
@@ -627,7 +615,53 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev):
     prof = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()}
     return ring_line(world=world, steps=K, warmup=args.warmup, per_step_s=per_step, nbytes=nbytes, dt_name=dt_name,
                      comm_info=info, rings=rings, mode=mode, tune_table=tune_table, prof=prof,
-                     ranks_share_gpu=share, cpu_baseline=cpu, extras=extras)
+                     ranks_share_gpu=share, cpu_baseline=cpu, extras=extras, calibration=calib)
+
+
+def reference_driven_leg(torch, dist, rank, world, device, nbytes) -> dict:
+    """The depth-A drop-in timed on this node (mccs_amd/refdrive.py): the
+    reference-named kernels driven exactly as plan.rs drives them, for the
+    configurations an unchanged Rust service selects by configuration alone.
+    Never fails the line (errors are recorded per variant)."""
+    from . import comm as C
+    from . import refdrive
+
+    t0 = time.perf_counter()
+    try:
+        rows = refdrive.time_reference_driven(torch, dist, rank, world, device, nbytes,
+                                              refdrive.default_variants(world, C.default_rings))
+    except Exception as e:  # noqa: BLE001
+        rows = [{"error": f"{type(e).__name__}: {e}"[:300]}]
+    torch.cuda.empty_cache()
+    return {"what": "reference-named kernels launched as plan.rs:602-669 does (grid = channels, block = "
+                    "get_task_schema threads, SHM-meta connector layout in IPC-shared device memory, "
+                    "host-mapped work ring, reference hand-off policy); fp32 exact-sum gated",
+            "bytes_per_rank": nbytes, "variants": rows, "wall_s": round(time.perf_counter() - t0, 2)}
+
+
+def node_legs(torch, C, world, ndev, nbytes):
+    """Rank 0 only: the one-process multi-device AllReduce (the reference's
+    service model) and the xGMI calibration, when this process sees `world`
+    distinct GPUs.  Returns (in_process dict, calibration dict or None)."""
+    from . import node_probe
+
+    if ndev < world:
+        na = {"n/a": f"this process sees {ndev} GPU(s) for {world} ranks (ranks share a GPU: no xGMI link)"}
+        return na, None
+    t0 = time.perf_counter()
+    try:
+        inproc = node_probe.in_process_multi_device(torch, C, world, nbytes)
+    except Exception as e:  # noqa: BLE001
+        inproc = {"error": f"{type(e).__name__}: {e}"[:300]}
+    inproc["wall_s"] = round(time.perf_counter() - t0, 2)
+    t0 = time.perf_counter()
+    try:
+        calib = node_probe.xgmi_calibration(torch, list(range(world)))
+    except Exception as e:  # noqa: BLE001
+        calib = {"error": f"{type(e).__name__}: {e}"[:300]}
+    calib["wall_s"] = round(time.perf_counter() - t0, 2)
+    torch.cuda.set_device(0)
+    return inproc, calib
 
 
 def setup2_jobs(world: int, interleaved: bool) -> list[list[int]]:
@@ -697,15 +731,41 @@ def setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup
             "jobs": out}
 
 
-def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False):
-    """BASELINE configs[4] alone: two concurrent trace jobs on the node.
-    value = sum of the jobs' algbw; ms_per_step = the slower job's mean
-    iteration time (compute gap + AllReduce + sync, traffic_gen's round
-    time).  MCCS_SETUP2_COMPUTE_SCALE scales the compute gaps (rehearsals)."""
-    scale = float(os.environ.get("MCCS_SETUP2_COMPUTE_SCALE", "1.0"))
-    res = setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, args.warmup, args.steps, scale)
-    if rank != 0:
-        return None
+def setup2_roofline(jobs, ranks_share_gpu: bool) -> dict:
+    """Roofline of the two-job line (value = the sum of the jobs' algbw).
+    Each job's per-rank link bytes 2(n-1)/n*S per call over its rings'
+    distinct outgoing links (n = 4: 3 links) at the spec rate; the line sums
+    achieved and peak over the jobs.  Ranks sharing one GPU (a rehearsal):
+    all jobs' (6n-4)*S algorithmic HBM bytes per call against that one HBM."""
+    from . import comm as C
+
+    per, ach, peak = [], 0.0, 0.0
+    for j in jobs:
+        n, s, t = j["ranks"], j["bytes"], j["ms_per_call"] / 1e3
+        if ranks_share_gpu:
+            a = (6 * n - 4) * s / t / 1e9
+            per.append({"job": j["job"], "bound": "hbm", "achieved": round(a, 2)})
+            ach += a
+            continue
+        links = out_links(C.default_rings(n), 0)
+        a = 2 * (n - 1) / n * s / t / 1e9
+        p = links * XGMI_LINK_GBPS_PER_DIR
+        per.append({"job": j["job"], "bound": "xgmi", "achieved": round(a, 2), "peak": round(p, 2),
+                    "frac": round(a / p, 4), "links": links})
+        ach += a
+        peak += p
+    if ranks_share_gpu:
+        peak = HBM_PEAK_GBPS
+    return {"bound": "hbm" if ranks_share_gpu else "xgmi", "achieved": round(ach, 2), "peak": round(peak, 2),
+            "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None,
+            "kernel": "ring_multi_kernel<AllReduce, half, Sum>", "per_job": per,
+            "note": ("ranks share one GPU: all jobs' (6n-4)*S algorithmic HBM bytes per call" if ranks_share_gpu
+                     else "per job: per-rank link bytes 2(n-1)/n*S per call over its distinct outgoing links x "
+                          f"{XGMI_LINK_GBPS_PER_DIR} GB/s per direction (spec); summed over the jobs")}
+
+
+def setup2_line(res, world, steps, warmup, scale, ranks_share_gpu, cpu_baseline) -> dict:
+    """The configs[4] line (pure: no GPU, unit-tested on CPU)."""
     jobs = res["jobs"]
     return {
         "metric": METRIC,
@@ -713,15 +773,36 @@ def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False
         "value": round(sum(j["algbw_GBps"] for j in jobs), 3),
         "unit": "GB/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        "steps": steps,
+        "warmup": warmup,
         "ms_per_step": max(j["iter_ms_mean"] for j in jobs),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f16",
         "data": "synthetic exact fp16 gradients per rank and iteration, device-resident buckets",
-        "config": {**res, "compute_scale": scale},
-        "roofline": None,
-        "cpu_baseline": None,
+        "config": {**res, "compute_scale": scale, "ranks_share_gpu": ranks_share_gpu},
+        "roofline": setup2_roofline(jobs, ranks_share_gpu),
+        "cpu_baseline": cpu_baseline,
     }
+
+
+def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False, cpu_sum_baseline=None):
+    """BASELINE configs[4] alone: two concurrent trace jobs on the node.
+    value = sum of the jobs' algbw; ms_per_step = the slower job's mean
+    iteration time (compute gap + AllReduce + sync, traffic_gen's round
+    time, traffic_gen/src/main.rs:167-228).  MCCS_SETUP2_COMPUTE_SCALE
+    scales the compute gaps (rehearsals).  cpu_baseline: the host sum of the
+    larger job's buckets (4 x setup-2_vgg fp16, sampled)."""
+    scale = float(os.environ.get("MCCS_SETUP2_COMPUTE_SCALE", "1.0"))
+    res = setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, args.warmup, args.steps, scale)
+    share = torch.cuda.device_count() < world
+    if rank != 0:
+        dist.barrier()
+        return None
+    cpu = None
+    if not getattr(args, "no_cpu_baseline", False) and cpu_sum_baseline is not None:
+        name, count = SETUP2_JOBS[0]
+        cpu = cpu_sum_baseline(len(setup2_jobs(world, interleaved)[0]), 2 * count, 6)
+    dist.barrier()
+    return setup2_line(res, world, args.steps, args.warmup, scale, share, cpu)

@@ -68,7 +68,7 @@ def main():
                                          ring_orders=ring_used)
                 got = vnode.from_dev(recv, code)
                 ok = bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8))) and not rr.aborted()
-                ok = ok and nthr == 544 and all(a == rr.chan_next[c] for c, a in enumerate(rr.done_acks()))
+                ok = ok and nthr == 544 and all(a == rr.ring.chan_next[c] for c, a in enumerate(rr.done_acks()))
                 if code == 2:
                     ok = ok and int(exp[0]) == 2042 * n + n * (n - 1) // 2
                 results[f"{vname}/dtype{code}/n{count}/rep{rep}"] = {"ok": ok, "steps": rr.steps()}
@@ -84,7 +84,7 @@ def main():
             rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, 2, 0, stream.cuda_stream)
         stream.synchronize()
         got = vnode.from_dev(recv, 2)
-        ok = bool(np.all(got == 2042 * n + n * (n - 1) // 2)) and not rr.aborted() and rr.next_available > 1024
+        ok = bool(np.all(got == 2042 * n + n * (n - 1) // 2)) and not rr.aborted() and rr.ring.next_available > 1024
         results[f"{vname}/wrap1100"] = {"ok": ok, "steps": rr.steps()}
         rr.close(dist.barrier)
     allres = allgather(results)

@@ -3,6 +3,7 @@ import json
 
 import pytest
 
+import bench
 from mccs_amd import comm as C
 from mccs_amd import ring_bench as rb
 
@@ -39,7 +40,7 @@ def _line(share, cpu=True):
                         comm_info={"channels": 7, "lanes": 9, "block_threads": 576},
                         rings=C.default_rings(8), mode="receiver-uncached-fifo", tune_table=[], prof={},
                         ranks_share_gpu=share,
-                        cpu_baseline=rb.cpu_sum_baseline(2, 1 << 20, budget_s=0.2) if cpu else None)
+                        cpu_baseline=bench.ring_cpu_baseline(2, 1 << 20, budget_s=0.2) if cpu else None)
 
 
 @pytest.mark.parametrize("share", [False, True])
@@ -115,3 +116,58 @@ def test_candidates_stay_within_coresident_workgroups():
         for _, cfg in modes:
             if cfg.channel_count and cfg.lanes:
                 assert cfg.channel_count * cfg.lanes <= rb.MAX_RING_WORKGROUPS
+
+
+def _setup2_res():
+    return {"workload": "w", "semantics": "s", "jobs": [
+        {"job": "setup-2_vgg", "ranks": 4, "global_ranks": [0, 1, 2, 3], "bytes": 574_668_960, "iterations": 10,
+         "iter_ms_mean": 170.0, "ms_per_call": 9.0, "algbw_GBps": 574_668_960 / 9e-3 / 1e9},
+        {"job": "setup-2_gpt_1", "ranks": 4, "global_ranks": [4, 5, 6, 7], "bytes": 83_886_080, "iterations": 10,
+         "iter_ms_mean": 8.0, "ms_per_call": 1.5, "algbw_GBps": 83_886_080 / 1.5e-3 / 1e9}]}
+
+
+@pytest.mark.parametrize("share", [False, True])
+def test_setup2_line_is_self_standing(share):
+    """configs[4] alone: value = the jobs' summed algbw, ms_per_step = the
+    slower job's round, an xGMI roofline summed over the jobs (HBM when the
+    ranks share one GPU) and a host cpu_baseline."""
+    cpu = bench.ring_cpu_baseline(2, 1 << 20, 6, budget_s=0.2)
+    d = rb.setup2_line(_setup2_res(), 8, 10, 1, 1.0, share, cpu)
+    for k in ("metric", "value", "unit", "n_gpus", "ms_per_step", "roofline", "cpu_baseline", "dtype", "config"):
+        assert d[k] is not None, k
+    assert d["ms_per_step"] == 170.0 and d["dtype"] == "f16"
+    rf = d["roofline"]
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and 0 < rf["frac"] <= 1
+    if share:
+        assert rf["bound"] == "hbm" and rf["peak"] == 8000.0
+    else:
+        assert rf["bound"] == "xgmi" and abs(rf["peak"] - 2 * 3 * rb.XGMI_LINK_GBPS_PER_DIR) < 1e-6  # 3 links per job rank
+        want = sum(2 * 3 / 4 * j["bytes"] / (j["ms_per_call"] / 1e3) / 1e9 for j in _setup2_res()["jobs"])
+        assert abs(rf["achieved"] - want) < 0.05
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] >= 1
+    json.dumps(d)
+
+
+def test_ring_line_carries_the_calibrated_peak_beside_the_spec():
+    calib = {"per_link_direction_GBps": 50.0}
+    d = rb.ring_line(world=8, steps=20, warmup=5, per_step_s=1.2e-3, nbytes=128 << 20, dt_name="float32",
+                     comm_info={}, rings=C.default_rings(8), mode="m", tune_table=[], prof={}, ranks_share_gpu=False,
+                     cpu_baseline=None, calibration=calib)
+    rf = d["roofline"]
+    assert rf["peak"] == 7 * rb.XGMI_LINK_GBPS_PER_DIR and rf["peak_calibrated"] == 350.0
+    assert abs(rf["frac_calibrated"] - rf["achieved"] / 350.0) < 1e-3
+    # sharing one GPU: no calibration fields (HBM-bound line)
+    d2 = rb.ring_line(world=8, steps=20, warmup=5, per_step_s=1.2e-3, nbytes=128 << 20, dt_name="float32",
+                      comm_info={}, rings=C.default_rings(8), mode="m", tune_table=[], prof={}, ranks_share_gpu=True,
+                      cpu_baseline=None, calibration=calib)
+    assert "peak_calibrated" not in d2["roofline"]
+
+
+def test_node_legs_report_na_when_ranks_share_a_gpu():
+    inproc, calib = rb.node_legs(None, C, world=8, ndev=1, nbytes=128 << 20)
+    assert "n/a" in inproc and calib is None
+
+
+def test_ring_cpu_baseline_samples_large_buckets():
+    cb = bench.ring_cpu_baseline(2, 1 << 30, 6, budget_s=0.2)
+    assert "first 256 MiB of the 1024 MiB bucket" in cb["sample"] and cb["value"] > 0
