@@ -65,11 +65,18 @@ def parse():
 
 
 def cpu_threads() -> int:
+    """Threads of the host-CPU baseline: this process's CPU share.  The GPU
+    box exposes every hardware thread of the host (256) to each job but
+    grants a share of 16 (OMP_NUM_THREADS, which `nproc` also honours);
+    the baseline runs on that share, not on CPUs other jobs own."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, n)  # every hardware thread this process may run on (the GPU box pins a 16-thread share)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
 
 
 def cpu_baseline(dtype_code: int, nelem: int, budget_s: float) -> dict:

@@ -337,7 +337,8 @@ mccsResult_t comm_stream(Comm* c, hipStream_t* out) {
 mccsResult_t comm_make_event_ipc(Comm* c) {
   if (c->event_ipc) return mccsSuccess;
   DeviceGuard g(c->device);
-  MCCS_HIP(hipEventSynchronize(c->event));
+  if (c->event_recorded) MCCS_HIP(hipEventSynchronize(c->event));
+  else MCCS_HIP(hipDeviceSynchronize());  // the latest launches recorded no event
   hipEvent_t e = nullptr;
   MCCS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess));
   (void)hipEventDestroy(c->event);
@@ -353,7 +354,8 @@ mccsResult_t comm_free(Comm* c) {
     g_live_fifo_slots.erase(c->d_comm);
   }
   // the last launch (any stream) must be done before its arenas are reused
-  if (c->event) (void)rt().EventSynchronize(c->event);
+  if (c->event_recorded) (void)rt().EventSynchronize(c->event);
+  else (void)rt().DeviceSynchronize();
   if (c->stream) (void)rt().StreamSynchronize(c->stream);
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
     if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)hipIpcCloseMemHandle(c->peer_arena[r]);

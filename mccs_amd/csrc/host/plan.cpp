@@ -147,7 +147,18 @@ struct LaunchDesc {
   uint64_t mask = 0;
   int nch_used = 0;
   mccsDevWork* work = nullptr;
+  bool work_inline = false;  // works in the launch arguments: no FIFO entry, no acknowledgement
 };
+
+// MCCS_EAGER_EVENTS=1: record the comm event after every launch (round-2
+// behaviour; A/B and callers that poll the event themselves).
+static bool eager_events() {
+  static const bool on = [] {
+    const char* v = std::getenv("MCCS_EAGER_EVENTS");
+    return v && std::atoi(v) != 0;
+  }();
+  return on;
+}
 
 // A launch being captured into a HIP graph: its works go to the comm's
 // graph arena, laid out like one FIFO upload (first work of channel i at
@@ -222,6 +233,7 @@ static mccsResult_t upload_work_inline(Comm* c, LaunchDesc* ld, mccsMultiLaunchA
   ld->mask = mask;
   ld->nch_used = (int)n;
   ld->work = nullptr;
+  ld->work_inline = true;
   ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
   ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
   for (auto& s : c->sched) s = ChannelSchedule{};
@@ -402,14 +414,21 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     }
     void* args[1] = {&ma};
     MCCS_HIP(rt().LaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, st));
-    MCCS_HIP(rt().EventRecord(c0->event, st));
+    // The comm events are recorded only when consumed (Comm::event_recorded):
+    // cross-stream ordering, an exported backend event, or a work-FIFO launch
+    // (wait_work_queue queries the event to tell a stuck kernel from a slow one).
+    bool record = events || !lds[0].work_inline || eager_events();
+    for (size_t k = 0; k < idx.size() && !record; ++k) record = comms[idx[k]]->event_ipc;
+    if (record) MCCS_HIP(rt().EventRecord(c0->event, st));
     if (events) {
       for (size_t k = 0; k < idx.size(); ++k) {
         if (!bridge && k == 0) continue;
         MCCS_HIP(rt().StreamWaitEvent(user_streams[idx[k]], c0->event));
       }
     }
-    for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
+    if (record)
+      for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
+    for (size_t k = 0; k < idx.size(); ++k) comms[idx[k]]->event_recorded = record;
   }
   return mccsSuccess;
 }

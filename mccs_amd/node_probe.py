@@ -124,7 +124,9 @@ def xgmi_calibration(torch, devices, nbytes: int = 64 << 20, reps: int = 10) -> 
     per stream after a warm-up) with one side of the copy on a peer GPU.
     `devices[0]` is the local GPU.  Uses mccs_hip_reduce_copy with the
     register streaming loop (the access pattern of the ring's reduce-copy)."""
-    from . import reduce as R
+    import importlib
+
+    R = importlib.import_module(__package__ + ".reduce")  # the module (the package exports a function `reduce`)
 
     devices = list(devices)
     nd = len(devices)

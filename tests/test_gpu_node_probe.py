@@ -22,7 +22,9 @@ def test_in_process_multi_device_code_path():
 def test_xgmi_calibration_code_path():
     import torch
 
-    from mccs_amd import reduce as R
+    import importlib
+
+    R = importlib.import_module("mccs_amd.reduce")
 
     before = R.get_tune()
     r = node_probe.xgmi_calibration(torch, [0, 0, 0], nbytes=4 << 20, reps=2)

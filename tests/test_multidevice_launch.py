@@ -225,3 +225,41 @@ def test_external_launch_refuses_blocks_without_a_control_wave():
     invalid_argument, allreduce = 4, 4  # mccsInvalidArgument, mccsFuncAllReduce
     assert f(allreduce, F32, SUM, 0x1000, 1, 0x2000, 1, 64, None) == invalid_argument
     assert f(allreduce, F32, SUM, 0x1000, 1, 0x2000, 1, 608, None) == invalid_argument
+
+
+def test_comm_events_recorded_only_when_consumed(fake, monkeypatch):
+    """A launch records the communicator event only when something consumes
+    it (plan.cpp; each record is a marker packet behind the kernel, ~5 us of
+    device time per call measured on MI355X): not for launch-argument works
+    on the caller's stream; yes for work-FIFO launches (wait_work_queue polls
+    the event), the two-stream bridge and MCCS_EAGER_EVENTS=1.  mccsCommSync
+    then waits on the event, or on the whole device when none was recorded."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
+    try:
+        _log()
+        _allreduce_group(comms)  # 7 inline works per rank
+        ev = _log()
+        assert not any(k == "record" for k, _ in ev), ev
+        for c in comms:
+            c.sync()
+        waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
+        assert waits.count("device") == 8 and "event" not in waits, waits
+        monkeypatch.setenv("MCCS_INLINE_WORKS", "0")  # the work FIFO: recorded
+        _allreduce_group(comms)
+        assert sum(1 for k, _ in _log() if k == "record") == 8
+        for c in comms:
+            c.sync()
+        waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
+        assert waits.count("event") == 8 and "device" not in waits, waits
+    finally:
+        for c in comms:
+            c.destroy()
+    comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20, bridge_streams=1))
+    try:
+        _log()
+        _allreduce_group(comms)
+        assert sum(1 for k, _ in _log() if k == "record") >= 8  # user events + comm events
+    finally:
+        for c in comms:
+            c.destroy()
