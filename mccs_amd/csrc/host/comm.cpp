@@ -25,9 +25,14 @@ namespace mccs {
 
 // ---------------------------------------------------------------------------
 // Ring patterns.  Default topology for one fully connected MI355X node:
-// edge-disjoint Hamiltonian cycles of K_n (greedy DFS, deterministic so every
-// rank derives the same rings), each used in both directions, so the rings
-// spread over n-2 or n-1 of the n-1 xGMI links of every GPU instead of one.
+//   n = 8: 7 arc-disjoint directed Hamiltonian cycles (every GPU sends and
+//          receives on all 7 of its xGMI links, one ring per link and
+//          direction);
+//   n = 4: all 6 directed Hamiltonian cycles (each link carries two);
+//   other n: edge-disjoint Hamiltonian cycles of K_n (greedy DFS,
+//          deterministic so every rank derives the same rings), each used in
+//          both directions: n-2 or n-1 of a GPU's n-1 links;
+//   n = 2: the one ring, 4 channels of it (below).
 static bool ham_dfs(int n, std::vector<std::vector<char>>& used, std::vector<int>& path,
                     std::vector<char>& seen) {
   if ((int)path.size() == n) return !used[path.back()][path[0]];
