@@ -129,7 +129,9 @@ def _candidates(C, lanes_opts, locs, chan_opts=(None,)):
             for lanes in lanes_opts:
                 if nch and lanes and nch * lanes > MAX_RING_WORKGROUPS:
                     continue
-                kw = dict(locality=loc, lanes=lanes, timeout_ms=60000)
+                # a correct 128 MiB AllReduce takes milliseconds: a mode whose hand-off
+                # fails over this node's links is caught by the watchdog within 20 s
+                kw = dict(locality=loc, lanes=lanes, timeout_ms=20000)
                 if nch:
                     kw["channel_count"] = nch
                 tag = f"{lname}/lanes={lanes or 'auto'}" + (f"/channels={nch}" if nch else "")
