@@ -330,10 +330,12 @@ def extra_allgather(torch, dist, C, comm, rank, world, dev, mib=16, warmup=3, K=
 SWEEP_BYTES = (32768, 131072, 524288, 2097152, 8388608, 33554432, 134217728, 536870912)
 
 
-def size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20):
+def size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20, graph_upto=8 << 20):
     """fp16 AllReduce latency / algbw / busbw over the reference's eval sizes
     (allreduce_bench semantics: algbw = bytes / t, busbw = algbw * 2(n-1)/n),
-    each size exact-sum validated."""
+    each size exact-sum validated.  Up to `graph_upto` bytes the same call
+    is also timed captured in a HIP graph (graph_latency_us): the eager path's
+    overhead over the device-side time."""
     rows = []
     for nb in SWEEP_BYTES:
         n = nb // 2
@@ -344,12 +346,27 @@ def size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20):
             C.all_reduce(comm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum)
 
         el = max_over_ranks(dist, time_steps(torch, dist, comm, step, warmup, K)) / K
+        gl = None
+        if nb <= graph_upto:
+            # 10 captured calls per size: a work-FIFO communicator (e.g. doubled
+            # channels) takes graph-arena entries per captured call (2048 in all)
+            try:
+                gl = graph_replay(torch, dist, comm, lambda st: C.all_reduce(
+                    comm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum, st), calls=10)
+            except Exception as e:  # noqa: BLE001  (informational column only)
+                print(f"[rank {rank}] sweep graph replay {nb} B: {e}", flush=True)
+                gl = None
+            gl = max_over_ranks(dist, gl if gl is not None else -1.0)
+            gl = gl if gl > 0 else None
         del x, y
         require(dist, exact_sum_ok(torch, C, comm, rank, world, n, torch.float16, C.AllReduceDataType.Float16, dev),
                 f"size sweep {nb} B")
         algbw = nb / el / 1e9
-        rows.append({"bytes": nb, "latency_us": round(el * 1e6, 2), "algbw_GBps": round(algbw, 3),
-                     "busbw_GBps": round(algbw * 2 * (world - 1) / world, 3), "exact": True})
+        row = {"bytes": nb, "latency_us": round(el * 1e6, 2), "algbw_GBps": round(algbw, 3),
+               "busbw_GBps": round(algbw * 2 * (world - 1) / world, 3), "exact": True}
+        if gl is not None:
+            row["graph_latency_us"] = round(gl * 1e6, 2)
+        rows.append(row)
     return rows
 
 
