@@ -167,21 +167,34 @@ class RefDrivenRank:
         self._dev_allocs, self._host_allocs, self._opened = [], [], []
         # -- connector memory: [SendBufMeta][RecvBufMeta][FIFO] per channel, one allocation
         self.stride = 2 * META + buff_size
-        mine, handle = ctypes.c_void_p(), (ctypes.c_char * 64)()
-        L.check(self.lib.mccsMemAllocShared(device, self.stride * nch, ctypes.byref(mine), handle),
-                "mccsMemAllocShared")
-        self._mine = mine.value
-        _ok(h.hipMemset(self._mine, 0, self.stride * nch), "hipMemset")
-        handles = allgather(bytes(handle))
+        self._mine = 0
+        # every rank joins the handle exchange even after a local failure (an
+        # empty handle), so a peer's error never leaves the others blocked in it
+        mine, handle, local_err = ctypes.c_void_p(), (ctypes.c_char * 64)(), None
+        try:
+            L.check(self.lib.mccsMemAllocShared(device, self.stride * nch, ctypes.byref(mine), handle),
+                    "mccsMemAllocShared")
+            self._mine = mine.value
+            _ok(h.hipMemset(self._mine, 0, self.stride * nch), "hipMemset")
+        except Exception as e:  # noqa: BLE001
+            local_err = e
+        handles = allgather(b"" if local_err else bytes(handle))
+        if local_err or any(not x for x in handles):
+            self.close()
+            raise RuntimeError(f"reference-driven connector setup failed ({local_err or 'on another rank'})")
         self.base = [0] * n
-        for r in range(n):
-            if r == rank:
-                self.base[r] = self._mine
-                continue
-            p = ctypes.c_void_p()
-            L.check(self.lib.mccsMemOpenShared(device, handles[r], ctypes.byref(p)), "mccsMemOpenShared")
-            self.base[r] = p.value
-            self._opened.append(p.value)
+        try:
+            for r in range(n):
+                if r == rank:
+                    self.base[r] = self._mine
+                    continue
+                p = ctypes.c_void_p()
+                L.check(self.lib.mccsMemOpenShared(device, handles[r], ctypes.byref(p)), "mccsMemOpenShared")
+                self.base[r] = p.value
+                self._opened.append(p.value)
+        except Exception:
+            self.close()  # no collective here: the caller agrees on the failure
+            raise
         # -- host-mapped sync: work ring + workFifoDone (device.rs:56-64)
         self.h_work, self.d_work = self._host_mapped(abi.MCCS_WORK_SIZE * WORK_DEPTH)
         self.h_done, self.d_done = self._host_mapped(4 * abi.MCCS_MAX_NCHANNELS)
@@ -323,8 +336,14 @@ class RefDrivenRank:
 
     def close(self, barrier=None) -> None:
         """Unmaps the peers' memory; `barrier()` (all ranks) before freeing our
-        own, which the peers may still have mapped."""
+        own, which the peers may still have mapped.  Safe on a partly built
+        rank."""
         h = hip()
+        for name in ("_opened", "_dev_allocs", "_host_allocs"):
+            if not hasattr(self, name):
+                setattr(self, name, [])
+        if not hasattr(self, "_mine"):
+            self._mine = 0
         h.hipDeviceSynchronize()
         for p in self._opened:
             self.lib.mccsMemCloseShared(self.device, ctypes.c_void_p(p))
@@ -407,45 +426,70 @@ def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbyte
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         return float(t.item())
 
+    def agree(ok: bool) -> bool:
+        return max_over_ranks(0.0 if ok else 1.0) == 0.0
+
+    # Every rank runs the same sequence of collectives whatever fails
+    # locally: a failure is recorded, agreed on, and the variant skipped on
+    # all ranks together.
     out = []
     for v in variants:
         res = {"variant": v["name"], "channels": v["nch"], "locality": v["locality"]}
-        rr = None
+        rr, err = None, None
         try:
             rr = RefDrivenRank(rank, world, device, allgather, nch=v["nch"], rings=v["rings"],
                                locality=v["locality"])
-            barrier()
-            recv.zero_()
-            torch.cuda.synchronize(dev)
-            rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
-            stream.synchronize()
-            k, nthr, _ = rr.last_plan
-            ok = bool(torch.equal(recv, want)) and not rr.aborted()
-            ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
-            res.update(grid=k, block=nthr, exact=ok)
-            if ok:
-                for _ in range(warmup):
-                    rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
-                stream.synchronize()
+        except Exception as e:  # noqa: BLE001
+            err = f"setup: {type(e).__name__}: {e}"[:300]
+        if agree(err is None):
+            try:
+                recv.zero_()
+                torch.cuda.synchronize(dev)
                 barrier()
-                t0 = time.perf_counter()
-                for _ in range(steps):
-                    rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+                rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
                 stream.synchronize()
-                el = max_over_ranks(time.perf_counter() - t0)
-                ok2 = bool(torch.equal(recv, want)) and not rr.aborted()
-                ok2 = max_over_ranks(0.0 if ok2 else 1.0) == 0.0
-                ms = el / steps * 1e3
-                res.update(ms_per_allreduce=round(ms, 4), algbw_GBps=round(nbytes / (ms * 1e-3) / 1e9, 2),
-                           busbw_GBps=round(nbytes / (ms * 1e-3) / 1e9 * 2 * (world - 1) / world, 2),
-                           exact_after_timing=ok2, steps=steps)
-        except Exception as e:  # recorded, never fatal to the caller's line
-            res["error"] = f"{type(e).__name__}: {e}"[:300]
-        finally:
-            if rr is not None:
+                k, nthr, _ = rr.last_plan
+                res.update(grid=k, block=nthr)
+                ok = bool(torch.equal(recv, want)) and not rr.aborted()
+            except Exception as e:  # noqa: BLE001  (a refused launch: the peers' kernels hit the watchdog)
+                err, ok = f"gate: {type(e).__name__}: {e}"[:300], False
+            ok = agree(ok)
+            res["exact"] = ok
+            if ok:
+                el = float("inf")
                 try:
-                    rr.close(barrier)
-                except Exception as e:
-                    res.setdefault("error", f"close: {e}"[:300])
+                    for _ in range(warmup):
+                        rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+                    stream.synchronize()
+                except Exception as e:  # noqa: BLE001
+                    err = f"warmup: {type(e).__name__}: {e}"[:300]
+                barrier()
+                try:
+                    t0 = time.perf_counter()
+                    for _ in range(steps):
+                        rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+                    stream.synchronize()
+                    el = time.perf_counter() - t0
+                    ok2 = bool(torch.equal(recv, want)) and not rr.aborted()
+                except Exception as e:  # noqa: BLE001
+                    err, ok2 = f"timing: {type(e).__name__}: {e}"[:300], False
+                el = max_over_ranks(el)
+                ok2 = agree(ok2)
+                res["exact_after_timing"] = ok2
+                if ok2 and el != float("inf"):
+                    ms = el / steps * 1e3
+                    res.update(ms_per_allreduce=round(ms, 4),
+                               algbw_GBps=round(nbytes / (ms * 1e-3) / 1e9, 2),
+                               busbw_GBps=round(nbytes / (ms * 1e-3) / 1e9 * 2 * (world - 1) / world, 2),
+                               steps=steps)
+        if err:
+            res["error"] = err
+        try:
+            if rr is not None:
+                rr.close(barrier)
+            else:
+                barrier()  # the peers' close() waits here before freeing
+        except Exception as e:  # noqa: BLE001
+            res.setdefault("error", f"close: {e}"[:300])
         out.append(res)
     return out
