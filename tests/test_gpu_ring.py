@@ -669,3 +669,33 @@ def test_allgather_captured_in_hip_graph(orc):
     finally:
         torch.cuda.synchronize()
         vnode.destroy(comms)
+
+
+def test_zero_count_collectives_are_noops_and_keep_fifo_steps(orc):
+    """count = 0 (an empty bucket): mccsAllReduce / mccsAllGather return
+    success without launching, inside and outside a group; the FIFO steps are
+    untouched, so the next AllReduce on the same communicators is still
+    bit-exact (n = 8, fewer elements than ranks next)."""
+    import torch
+
+    n = 8
+    comms = C.init_all([0] * n)
+    try:
+        x = [torch.ones(4, device="cuda") for _ in range(n)]
+        y = [torch.full((4,), 7.0, device="cuda") for _ in range(n)]
+        with C.group():
+            for r in range(n):
+                C.all_reduce(comms[r], x[r], y[r], 0, F32, 0)
+        for r in range(n):
+            C.all_gather(comms[r], x[r], y[r], 0)  # outside a group: nothing to launch either
+        for c in comms:
+            c.sync()
+        assert all(bool(torch.all(t == 7.0)) for t in y)
+        rng = np.random.default_rng(3)
+        for count in (3, 100003):
+            inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
+            outs = vnode.run_allreduce(comms, inputs, F32, 0)
+            exp = vnode.expected_allreduce(orc, inputs, F32, 0, comms[0])
+            _check_all_equal(outs, exp, F32)
+    finally:
+        vnode.destroy(comms)
