@@ -230,7 +230,6 @@ class RefDrivenRank:
             ch.workFifoDone = self.d_done + 4 * c
         self.d_comm = self._upload(bytes(hc))
         # -- planner state (plan.rs)
-        self.load = [0] * nch
         self.ring = WorkRing(nch)
         self.launches = 0
         self._works = {}
@@ -278,11 +277,12 @@ class RefDrivenRank:
         sch, nthr = ctypes.c_int(), ctypes.c_int()
         self.lib.mccs_task_schema(nbytes, self.nch, ctypes.byref(sch), ctypes.byref(nthr))
         k, nthr = sch.value, nthr.value
-        # select_best_channels (plan.rs:292-302): least loaded first; blocks
-        # map to the set bits of channelMask in ascending channel order
-        chans = sorted(sorted(range(self.nch), key=lambda i: (self.load[i], i))[:k])
-        for c in chans:
-            self.load[c] += nbytes
+        # select_best_channels (plan.rs:292-302): least loaded first, ties by
+        # id; the loads belong to the plan being built (one task per plan
+        # here), so they start at zero: channels 0..k-1, which also map to the
+        # set bits of channelMask in ascending order
+        load = [0] * self.nch
+        chans = sorted(sorted(range(self.nch), key=lambda i: (load[i], i))[:k])
         mask_q = WORK_DEPTH - 1
         start, acks = self.ring.reserve(chans, self._read_done, self._write_done)
         key = (send_ptr, recv_ptr, count, k, nthr)
