@@ -666,7 +666,7 @@ def node_legs(torch, C, world, ndev, nbytes):
 
     if ndev < world:
         na = {"n/a": f"this process sees {ndev} GPU(s) for {world} ranks (ranks share a GPU: no xGMI link)"}
-        return na, None
+        return na, dict(na)
     t0 = time.perf_counter()
     try:
         inproc = node_probe.in_process_multi_device(torch, C, world, nbytes)

@@ -165,7 +165,12 @@ def test_ring_line_carries_the_calibrated_peak_beside_the_spec():
 
 def test_node_legs_report_na_when_ranks_share_a_gpu():
     inproc, calib = rb.node_legs(None, C, world=8, ndev=1, nbytes=128 << 20)
-    assert "n/a" in inproc and calib is None
+    assert "n/a" in inproc and "n/a" in calib
+    # an n/a calibration leaves the spec-priced roofline alone
+    d = rb.ring_line(world=8, steps=20, warmup=5, per_step_s=1.2e-3, nbytes=128 << 20, dt_name="float32",
+                     comm_info={}, rings=C.default_rings(8), mode="m", tune_table=[], prof={}, ranks_share_gpu=False,
+                     cpu_baseline=None, extras={"xgmi_calibration": calib}, calibration=calib)
+    assert "peak_calibrated" not in d["roofline"] and "n/a" in d["config"]["xgmi_calibration"]
 
 
 def test_ring_cpu_baseline_samples_large_buckets():
