@@ -47,6 +47,8 @@ def main():
         dist.all_gather_object(out, obj)
         return out
 
+    if os.environ.get("REFDRV_BIG") == "1":
+        return big_case(torch, dist, refdrive, orc, rank, n, dev, allgather)
     rot = list(range(1, n)) + [0]
     variants = [("ref_sender", 2, None, "sender"), ("rotated_receiver", 2, [rot, rot[::-1]], "receiver")]
     results = {}
@@ -95,6 +97,52 @@ def main():
             merged[k] = all(r[k]["ok"] for r in allres) and all(s == steps[0] for s in steps)
         print(json.dumps({"world": n, "cases": merged, "all_ok": all(merged.values()),
                           "final_steps": allres[0][k]["steps"]}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def big_case(torch, dist, refdrive, orc, rank, n, dev, allgather):
+    """configs[2]'s bucket (128 MiB fp32 per rank), random uniform [-1, 1)
+    inputs, reference-driven at the mccs.toml default (2 channels, ring
+    0..n-1) and at 32 channels: every rank's output bit for bit against the
+    oracle's ring order.  Each process regenerates every rank's inputs from
+    the same seeds (no bulk exchange)."""
+    import numpy as np
+
+    count = (128 << 20) // 4
+    g = torch.Generator(device="cuda")
+
+    def inputs_of(r):
+        g.manual_seed(9100 + r)
+        return torch.rand(count, device="cuda", generator=g) * 2 - 1
+
+    mine = inputs_of(rank)
+    host = [inputs_of(r).cpu().numpy() for r in range(n)]
+    stream = torch.cuda.Stream()
+    results = {}
+    for nch in (2, 32):
+        rr = refdrive.RefDrivenRank(rank, n, dev, allgather, nch=nch)
+        recv = torch.empty_like(mine)
+        torch.cuda.synchronize()
+        dist.barrier()
+        rr.all_reduce(mine.data_ptr(), recv.data_ptr(), count, 7, 0, stream.cuda_stream)
+        stream.synchronize()
+        k, nthr, rings = rr.last_plan
+        want = orc.ring_allreduce_mt(7, 0, host, nchannels=k, nthreads=nthr, buff_size=rr.buff, ring_orders=rings,
+                                     workers=min(16, os.cpu_count() or 1))
+        got = recv.cpu().numpy()
+        naive = host[0].copy()
+        for r in range(1, n):
+            naive += host[r]
+        results[f"big/ch{nch}"] = {"ok": bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+                                   and not rr.aborted() and (n < 3 or not np.array_equal(naive, want)),
+                                   "steps": rr.steps(), "grid": k, "block": nthr}
+        rr.close(dist.barrier)
+    allres = allgather(results)
+    if rank == 0:
+        merged = {k: all(r[k]["ok"] for r in allres) for k in results}
+        print(json.dumps({"world": n, "cases": merged, "all_ok": all(merged.values()),
+                          "plans": {k: [results[k]["grid"], results[k]["block"]] for k in results}}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

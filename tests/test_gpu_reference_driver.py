@@ -29,11 +29,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_reference_driven_launch_matches_oracle(world):
+@pytest.mark.parametrize("world,big", [(2, False), (3, False), (3, True)], ids=["2", "3", "3-configs2-bucket"])
+def test_reference_driven_launch_matches_oracle(world, big):
+    """big: configs[2]'s 128 MiB fp32 bucket, random inputs, 2 and 32
+    channels (grid = channels, 544 threads), bit-exact at n = 3 where the
+    ring order matters (a rank-order sum differs: checked)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(HERE, "refdrv_worker.py")]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", REFDRV_BIG="1" if big else "0")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=os.path.dirname(HERE))
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
