@@ -122,7 +122,7 @@ def cpu_baseline(dtype_code: int, nelem: int, budget_s: float) -> dict:
 def ring_cpu_baseline(world: int, nbytes: int, dtype_code: int = 7, budget_s: float = 6.0) -> dict:
     """N > 1 lines: the host computes the AllReduce result itself -- the
     elementwise sum of `world` buckets of `nbytes` (oracle_reduce_mt, C,
-    pthreads) on every hardware thread this process may use, plus one
+    pthreads) on this process's CPU share (cpu_threads), plus one
     thread.  value = S / t, comparable with algbw; the host moved (n+1)*S
     bytes per pass.  A bucket larger than 256 MiB is sampled (its first
     256 MiB), so the leg stays within budget_s."""
