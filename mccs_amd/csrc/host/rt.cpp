@@ -295,8 +295,12 @@ unsigned rt_generation() { return g_generation.load(); }
 
 // ---- test-only C-ABI (tests/test_multidevice_launch.py) -------------------
 // Installs (ndevices > 0) or removes (0) the recording fake runtime.  Only
-// communicators created while it is installed may be used with it.
+// communicators created while it is installed may be used with it.  Refused
+// (mccsInvalidUsage) unless MCCS_TEST_HOOKS=1 is set in the environment, so
+// no production caller can swap the device runtime by accident.
 extern "C" mccsResult_t mccs_test_fake_runtime(int ndevices) {
+  const char* hooks = std::getenv("MCCS_TEST_HOOKS");
+  if (!hooks || std::atoi(hooks) != 1) return mccsInvalidUsage;
   if (ndevices < 0 || ndevices > 64) return mccsInvalidArgument;
   mccs::rt_use_fake(ndevices);
   return mccsSuccess;

@@ -28,14 +28,20 @@ def _parse(line):
 
 
 @pytest.fixture
-def fake():
+def fake(monkeypatch):
     lib = _lib.load()
+    monkeypatch.setenv("MCCS_TEST_HOOKS", "1")  # the hook is refused without it
 
     def install(ndev):
         assert lib.mccs_test_fake_runtime(ndev) == 0
 
     yield install
     lib.mccs_test_fake_runtime(0)
+
+
+def test_fake_runtime_hook_is_refused_without_opt_in(monkeypatch):
+    monkeypatch.delenv("MCCS_TEST_HOOKS", raising=False)
+    assert _lib.load().mccs_test_fake_runtime(4) == 5  # mccsInvalidUsage: HIP stays installed
 
 
 def _log(clear=True):
