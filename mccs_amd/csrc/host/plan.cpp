@@ -413,13 +413,22 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       ma.cfg.profile |= ck->kcfg.profile;
     }
     void* args[1] = {&ma};
-    MCCS_HIP(rt().LaunchKernel(lds[0].multi_fn, dim3(grid, (unsigned)idx.size()), dim3(block), args, st));
-    // The comm events are recorded only when consumed (Comm::event_recorded):
+    // The launching comm's event rides on the dispatch's own completion signal
+    // (hipExtLaunchKernel stopEvent): a hipEventRecord behind the kernel is a
+    // marker packet that cost ~3 us of device time per launch on MI355X, the
+    // stop event nothing (tools/launch_cost.hip).  Not while capturing (a
+    // graph replays plain kernel nodes) and not for an interprocess event
+    // (exported to a backend: recorded the usual way).
+    const bool stop_on_launch = !capturing && !c0->event_ipc;
+    const dim3 g3(grid, (unsigned)idx.size());
+    if (stop_on_launch) MCCS_HIP(rt().LaunchKernelExt(lds[0].multi_fn, g3, dim3(block), args, st, c0->event));
+    else MCCS_HIP(rt().LaunchKernel(lds[0].multi_fn, g3, dim3(block), args, st));
+    // Other events are recorded only when consumed (Comm::event_recorded):
     // cross-stream ordering, an exported backend event, or a work-FIFO launch
     // (wait_work_queue queries the event to tell a stuck kernel from a slow one).
     bool record = events || !lds[0].work_inline || eager_events();
     for (size_t k = 0; k < idx.size() && !record; ++k) record = comms[idx[k]]->event_ipc;
-    if (record) MCCS_HIP(rt().EventRecord(c0->event, st));
+    if (record && !stop_on_launch) MCCS_HIP(rt().EventRecord(c0->event, st));
     if (events) {
       for (size_t k = 0; k < idx.size(); ++k) {
         if (!bridge && k == 0) continue;
@@ -429,6 +438,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     if (record)
       for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
     for (size_t k = 0; k < idx.size(); ++k) comms[idx[k]]->event_recorded = record;
+    c0->event_recorded = record || stop_on_launch;
   }
   return mccsSuccess;
 }

@@ -3,6 +3,8 @@
 // GPUs.
 #include "rt.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -71,6 +73,10 @@ class HipRuntime final : public DeviceRuntime {
   }
   hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
     return hipLaunchKernel(fn, grid, block, args, 0, s);
+  }
+  hipError_t LaunchKernelExt(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s,
+                             hipEvent_t stop) override {
+    return hipExtLaunchKernel(fn, grid, block, args, 0, s, nullptr, stop, 0);
   }
   hipError_t BlocksPerCu(int* per_cu, const void* fn, int block) override {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, block, 0);
@@ -200,6 +206,13 @@ class FakeRuntime final : public DeviceRuntime {
     *capturing = false;
     return hipSuccess;
   }
+  hipError_t LaunchKernelExt(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s,
+                             hipEvent_t stop) override {
+    stop_ = stop;
+    const hipError_t e = LaunchKernel(fn, grid, block, args, s);
+    stop_ = nullptr;
+    return e;
+  }
   hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
     // every communicator of a fused ring launch must live on the launching device
     bool on_dev = true;
@@ -211,7 +224,7 @@ class FakeRuntime final : public DeviceRuntime {
     }
     note("launch dev=" + std::to_string(cur_) + " grid=" + std::to_string(grid.x) + "x" + std::to_string(grid.y) +
          " block=" + std::to_string(block.x) + " stream=" + sid(s) + " comms_on_dev=" + (on_dev ? "1" : "0") +
-         " inline_works=" + std::to_string(inl));
+         " inline_works=" + std::to_string(inl) + " stop_event=" + std::to_string((uintptr_t)stop_));
     return hipSuccess;
   }
   hipError_t BlocksPerCu(int* per_cu, const void*, int) override {
@@ -252,6 +265,7 @@ class FakeRuntime final : public DeviceRuntime {
     log_ << line << '\n';
   }
   int ndev_, cur_ = 0;
+  hipEvent_t stop_ = nullptr;  // the stop event of the launch being logged (LaunchKernelExt)
   uintptr_t next_id_ = 0;
   std::mutex mu_;
   std::map<void*, Block> mem_;

@@ -44,6 +44,10 @@ class DeviceRuntime {
   virtual hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) = 0;
   virtual hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) = 0;
   virtual hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) = 0;
+  // The same launch with `stop` recorded by the dispatch's own completion
+  // signal (hipExtLaunchKernel): no marker packet behind the kernel.
+  virtual hipError_t LaunchKernelExt(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s,
+                                     hipEvent_t stop) = 0;
   virtual hipError_t BlocksPerCu(int* per_cu, const void* fn, int block) = 0;
   virtual hipError_t CuCount(int* ncu, int device) = 0;
 };

@@ -8,6 +8,8 @@ namespace mccs {
 int comm_fifo_slots_of(const void* d_comm);  // host/comm.cpp
 }
 
+#include <hip/hip_ext.h>
+
 #include <mutex>
 #include <vector>
 
@@ -142,19 +144,31 @@ extern "C" mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, mccsDe
   std::lock_guard<std::mutex> lk(g_ext_mu);
   if (colocated_launch_running(device, comm)) return mccsInvalidUsage;
   void* args[3] = {&comm, &channelMask, &workHead};
-  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, stream);
-  if (e != hipSuccess) return mccsUnhandledCudaError;
-  // remember this launch until it completes (replacing this comm's previous one)
-  for (size_t i = 0; i < g_ext.size(); ++i)
-    if (g_ext[i].device == device && g_ext[i].comm == comm) {
-      (void)hipEventDestroy(g_ext[i].done);
-      g_ext.erase(g_ext.begin() + i);
-      break;
-    }
-  hipEvent_t done = nullptr;
-  if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
-      hipEventRecord(done, stream) != hipSuccess)
+  // the co-location guard's event rides on the dispatch's completion signal
+  // (no marker packet behind the kernel, tools/launch_cost.hip); a capturing
+  // stream gets a plain kernel node and a recorded event
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) != hipSuccess) return mccsUnhandledCudaError;
+  const bool capturing = cap == hipStreamCaptureStatusActive;
+  // this comm's entry (its latest launch) is reused eagerly: re-recording the
+  // event moves it to the newest launch, which is what the guard asks about
+  ExtLaunch* mine = nullptr;
+  for (auto& x : g_ext)
+    if (x.device == device && x.comm == comm) mine = &x;
+  hipEvent_t done = (mine && !capturing) ? mine->done : nullptr;
+  if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) return mccsUnhandledCudaError;
+  hipError_t e = capturing ? hipLaunchKernel(fn, dim3(grid), dim3(block), args, 0, stream)
+                           : hipExtLaunchKernel(fn, dim3(grid), dim3(block), args, 0, stream, nullptr, done, 0);
+  if (e == hipSuccess && capturing) e = hipEventRecord(done, stream);
+  if (e != hipSuccess) {
+    if (!mine || done != mine->done) (void)hipEventDestroy(done);
     return mccsUnhandledCudaError;
-  g_ext.push_back(ExtLaunch{device, comm, done});
+  }
+  if (mine && mine->done != done) {  // a captured launch replaced the entry's event
+    (void)hipEventDestroy(mine->done);
+    mine->done = done;
+  } else if (!mine) {
+    g_ext.push_back(ExtLaunch{device, comm, done});
+  }
   return mccsSuccess;
 }

@@ -233,31 +233,28 @@ def test_external_launch_refuses_blocks_without_a_control_wave():
     assert f(allreduce, F32, SUM, 0x1000, 1, 0x2000, 1, 608, None) == invalid_argument
 
 
-def test_comm_events_recorded_only_when_consumed(fake, monkeypatch):
-    """A launch records the communicator event only when something consumes
-    it (plan.cpp; each record is a marker packet behind the kernel, ~5 us of
-    device time per call measured on MI355X): not for launch-argument works
-    on the caller's stream; yes for work-FIFO launches (wait_work_queue polls
-    the event), the two-stream bridge and MCCS_EAGER_EVENTS=1.  mccsCommSync
-    then waits on the event, or on the whole device when none was recorded."""
+def test_comm_events_ride_on_the_launch(fake, monkeypatch):
+    """A communicator launch carries its comm event as the dispatch's stop
+    event (hipExtLaunchKernel): a hipEventRecord behind the kernel is a marker
+    packet that cost ~3 us of device time per launch on MI355X
+    (tools/launch_cost.hip).  mccsCommSync then waits on that event.  Extra
+    records remain only where something consumes them: the two-stream
+    bridge's user events."""
     fake(8)
     comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
     try:
         _log()
-        _allreduce_group(comms)  # 7 inline works per rank
-        ev = _log()
-        assert not any(k == "record" for k, _ in ev), ev
-        for c in comms:
-            c.sync()
-        waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
-        assert waits.count("device") == 8 and "event" not in waits, waits
-        monkeypatch.setenv("MCCS_INLINE_WORKS", "0")  # the work FIFO: recorded
-        _allreduce_group(comms)
-        assert sum(1 for k, _ in _log() if k == "record") == 8
-        for c in comms:
-            c.sync()
-        waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
-        assert waits.count("event") == 8 and "device" not in waits, waits
+        for inline in ("1", "0"):  # launch-argument works, then the work FIFO
+            monkeypatch.setenv("MCCS_INLINE_WORKS", inline)
+            _allreduce_group(comms)
+            ev = _log()
+            launches = [kv for k, kv in ev if k == "launch"]
+            assert len(launches) == 8 and all(kv["stop_event"] != "0" for kv in launches), launches
+            assert not any(k == "record" for k, _ in ev), ev
+            for c in comms:
+                c.sync()
+            waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
+            assert waits.count("event") == 8 and "device" not in waits, waits
     finally:
         for c in comms:
             c.destroy()
@@ -265,7 +262,31 @@ def test_comm_events_recorded_only_when_consumed(fake, monkeypatch):
     try:
         _log()
         _allreduce_group(comms)
-        assert sum(1 for k, _ in _log() if k == "record") >= 8  # user events + comm events
+        ev = _log()
+        assert sum(1 for k, _ in ev if k == "record") == 8  # the user events of the bridge
+        assert all(kv["stop_event"] != "0" for k, kv in ev if k == "launch")
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_fused_ranks_record_their_events_only_when_consumed(fake):
+    """Ranks sharing a device run as one launch: the first comm's event rides
+    on it; the others' events are recorded only when consumed (here: not), and
+    their mccsCommSync waits on the device instead."""
+    fake(4)
+    comms = C.init_all([0, 0, 1, 1, 2, 2, 3, 3], C.CommConfig(buffer_size=1 << 20, lanes=2, channel_count=1,
+                                                              rings=[[0, 1, 2, 3, 4, 5, 6, 7]]))
+    try:
+        _log()
+        _allreduce_group(comms)
+        ev = _log()
+        assert sum(1 for k, _ in ev if k == "launch") == 4
+        assert not any(k == "record" for k, _ in ev), ev
+        for c in comms:
+            c.sync()
+        waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
+        assert waits.count("event") == 4 and waits.count("device") == 4, waits
     finally:
         for c in comms:
             c.destroy()
