@@ -59,12 +59,13 @@ def _exact(torch, n, rank, dev):
 
 
 def in_process_multi_device(torch, C, world: int, nbytes: int, warmup: int = 3, steps: int = 10,
-                            devices=None) -> dict:
+                            devices=None, config=None) -> dict:
     """One process, `world` ranks on `devices` (default 0..world-1): exact-sum
-    gate, then `steps` grouped AllReduces of nbytes fp32 per rank."""
+    gate, then `steps` grouped AllReduces of nbytes fp32 per rank.  `config`:
+    the CommConfig (default: the library's)."""
     devices = list(devices if devices is not None else range(world))
     n = nbytes // 4
-    comms = C.init_all(devices)
+    comms = C.init_all(devices, config)
     try:
         xs, ys, sts = [], [], []
         for r, d in enumerate(devices):
@@ -98,7 +99,7 @@ def in_process_multi_device(torch, C, world: int, nbytes: int, warmup: int = 3, 
             ok = ok and bool(torch.equal(ys[r], (tot.to(torch.float64) / 64.0).to(torch.float32)))
             del tot
         res = {"devices": devices, "channels": comms[0].nchannels, "lanes": comms[0].lanes,
-               "exact_sum_full_size": ok}
+               "fifo_memory": comms[0].fifo_memory, "exact_sum_full_size": ok}
         if not ok:
             return res
         for _ in range(warmup):

@@ -617,7 +617,8 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
     if not getattr(args, "no_extra", False):
         # rank 0 alone drives every GPU; ranks 1..N-1 wait at the barrier below
         if rank == 0:
-            extras["in_process_multi_device"], calib = node_legs(torch, C, world, ndev, nbytes)
+            extras["in_process_multi_device"], calib = node_legs(torch, C, world, ndev, nbytes,
+                                                                 mode_config(C, mode, info))
             extras["xgmi_calibration"] = calib
         dist.barrier()
     if rank != 0:
@@ -658,10 +659,23 @@ def reference_driven_leg(torch, dist, rank, world, device, nbytes) -> dict:
             "bytes_per_rank": nbytes, "variants": rows, "wall_s": round(time.perf_counter() - t0, 2)}
 
 
-def node_legs(torch, C, world, ndev, nbytes):
+def mode_config(C, mode: str, info: dict):
+    """The CommConfig of the transport the line timed (its mode name, e.g.
+    "sender-uncached-fifo+release-fence", plus its channels and lanes), so a
+    leg can rerun the same transport through another deployment path."""
+    loc = C.LOCALITY_SENDER if (mode or "").startswith("sender") else C.LOCALITY_RECEIVER
+    kind = (mode or "").split("-", 1)[-1]
+    fifo = {"uncached-fifo": C.FIFO_UNCACHED, "uncached-fifo+release-fence": C.FIFO_UNCACHED_RELEASE,
+            "cached-fifo+system-fences": C.FIFO_DEVICE}.get(kind, C.FIFO_UNCACHED)
+    return C.CommConfig(channel_count=info.get("channels"), lanes=info.get("lanes"), locality=loc, fifo_memory=fifo,
+                        timeout_ms=20000)
+
+
+def node_legs(torch, C, world, ndev, nbytes, config=None):
     """Rank 0 only: the one-process multi-device AllReduce (the reference's
-    service model) and the xGMI calibration, when this process sees `world`
-    distinct GPUs.  Returns (in_process dict, calibration dict or None)."""
+    service model) with the transport the line timed (`config`), and the
+    xGMI calibration, when this process sees `world` distinct GPUs.  Returns
+    (in_process dict, calibration dict)."""
     from . import node_probe
 
     if ndev < world:
@@ -669,7 +683,7 @@ def node_legs(torch, C, world, ndev, nbytes):
         return na, dict(na)
     t0 = time.perf_counter()
     try:
-        inproc = node_probe.in_process_multi_device(torch, C, world, nbytes)
+        inproc = node_probe.in_process_multi_device(torch, C, world, nbytes, config=config)
     except Exception as e:  # noqa: BLE001
         inproc = {"error": f"{type(e).__name__}: {e}"[:300]}
     inproc["wall_s"] = round(time.perf_counter() - t0, 2)

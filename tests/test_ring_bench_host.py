@@ -163,6 +163,21 @@ def test_ring_line_carries_the_calibrated_peak_beside_the_spec():
     assert "peak_calibrated" not in d2["roofline"]
 
 
+@pytest.mark.parametrize("mode,loc,fifo", [
+    ("receiver-uncached-fifo", "LOCALITY_RECEIVER", "FIFO_UNCACHED"),
+    ("sender-uncached-fifo+release-fence", "LOCALITY_SENDER", "FIFO_UNCACHED_RELEASE"),
+    ("sender-cached-fifo+system-fences", "LOCALITY_SENDER", "FIFO_DEVICE")])
+def test_mode_config_reproduces_the_timed_transport(mode, loc, fifo):
+    cfg = rb.mode_config(C, mode, {"channels": 14, "lanes": 16})
+    assert cfg.locality == getattr(C, loc) and cfg.fifo_memory == getattr(C, fifo)
+    assert cfg.channel_count == 14 and cfg.lanes == 16
+    # every candidate mode name maps back to its own config
+    for _, modes in rb._candidates(C, [None], [C.LOCALITY_RECEIVER, C.LOCALITY_SENDER]):
+        for name, want in modes:
+            got = rb.mode_config(C, name, {})
+            assert (got.locality, got.fifo_memory) == (want.locality, want.fifo_memory), name
+
+
 def test_node_legs_report_na_when_ranks_share_a_gpu():
     inproc, calib = rb.node_legs(None, C, world=8, ndev=1, nbytes=128 << 20)
     assert "n/a" in inproc and "n/a" in calib
