@@ -378,21 +378,24 @@ def expected_exact(torch, count: int, world: int, dtype, device):
     return acc.to(dtype)
 
 
-def default_variants(world: int, default_rings) -> list[dict]:
+def default_variants(world: int, default_rings, max_channels: int = 32) -> list[dict]:
     """The configurations an unchanged service can run by configuration alone:
     mccs.toml's channel_count = 2 (the shipped default), MCCS_MAX_NCHANNELS =
     32 on the reference ring, and the same 32-channel budget over this
     library's link-spreading rings given as comm_patterns_override, with the
-    FIFO data at the sender (the reference SHM layout) or the receiver."""
+    FIFO data at the sender (the reference SHM layout) or the receiver.
+    `max_channels` caps the budget where ranks share one GPU (a rehearsal:
+    every rank's workgroups must be resident at once)."""
+    cap = max(2, min(32, max_channels))
     base = default_rings(world, 0)
     uniq = []
     for r in base:
         if r not in uniq:
             uniq.append(r)
-    spread = (uniq * 32)[:(32 // len(uniq)) * len(uniq)]
+    spread = (uniq * cap)[:max(1, cap // len(uniq)) * len(uniq)]
     return [
         {"name": "ch2_reference_ring_sender", "nch": 2, "rings": None, "locality": "sender"},
-        {"name": "ch32_reference_ring_sender", "nch": 32, "rings": None, "locality": "sender"},
+        {"name": f"ch{cap}_reference_ring_sender", "nch": cap, "rings": None, "locality": "sender"},
         {"name": f"ch{len(spread)}_spread_rings_sender", "nch": len(spread), "rings": spread, "locality": "sender"},
         {"name": f"ch{len(spread)}_spread_rings_receiver", "nch": len(spread), "rings": spread,
          "locality": "receiver"},

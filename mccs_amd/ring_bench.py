@@ -647,9 +647,13 @@ def reference_driven_leg(torch, dist, rank, world, device, nbytes) -> dict:
     from . import refdrive
 
     t0 = time.perf_counter()
+    # ranks sharing one GPU (a rehearsal): every rank's one-workgroup-per-
+    # channel kernel must be resident at once, so keep them to half the CUs
+    share = torch.cuda.device_count() < world
+    max_ch = max(2, 128 // world) if share else 32
     try:
         rows = refdrive.time_reference_driven(torch, dist, rank, world, device, nbytes,
-                                              refdrive.default_variants(world, C.default_rings))
+                                              refdrive.default_variants(world, C.default_rings, max_ch))
     except Exception as e:  # noqa: BLE001
         rows = [{"error": f"{type(e).__name__}: {e}"[:300]}]
     torch.cuda.empty_cache()

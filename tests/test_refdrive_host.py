@@ -118,5 +118,11 @@ def test_configuration_only_variants(n):
         assert len(uniq) == 7 and vs[2]["nch"] == 28
 
 
+def test_variants_capped_when_ranks_share_a_gpu():
+    vs = refdrive.default_variants(8, C.default_rings, 16)
+    assert [v["nch"] for v in vs] == [2, 16, 14, 14]
+    assert all(v["nch"] * 8 <= 128 for v in vs)
+
+
 def test_reference_rings_are_the_engine_default():
     assert refdrive.reference_rings(4, 2) == [[0, 1, 2, 3], [0, 1, 2, 3]]

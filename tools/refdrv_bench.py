@@ -36,8 +36,9 @@ def main():
     dev = int(os.environ.get("LOCAL_RANK", rank)) % ndev
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    max_ch = max(2, 128 // world) if ndev < world else 32  # ranks sharing a GPU: half the CUs
     res = refdrive.time_reference_driven(torch, dist, rank, world, dev, a.mib << 20,
-                                         refdrive.default_variants(world, C.default_rings),
+                                         refdrive.default_variants(world, C.default_rings, max_ch),
                                          warmup=a.warmup, steps=a.steps)
     if rank == 0:
         print(json.dumps({"tool": "refdrv_bench", "world": world, "ranks_share_gpu": ndev < world,
