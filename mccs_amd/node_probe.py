@@ -25,6 +25,8 @@ from __future__ import annotations
 import ctypes
 import time
 
+from ._streams import side_stream
+
 
 def _hip():
     from .refdrive import hip
@@ -72,7 +74,7 @@ def in_process_multi_device(torch, C, world: int, nbytes: int, warmup: int = 3, 
             dev = torch.device("cuda", d)
             xs.append((_exact(torch, n, r, dev).to(torch.float32) / 64.0))
             ys.append(torch.empty_like(xs[-1]))
-            sts.append(torch.cuda.Stream(device=dev))
+            sts.append(side_stream(torch, d, slot=0))
         for d in set(devices):
             torch.cuda.synchronize(d)
 
@@ -121,14 +123,17 @@ def in_process_multi_device(torch, C, world: int, nbytes: int, warmup: int = 3, 
 
 
 def xgmi_calibration(torch, devices, nbytes: int = 64 << 20, reps: int = 10) -> dict:
-    """Copy bandwidth (GB/s of bytes copied, wall time over `reps` launches
-    per stream after a warm-up) with one side of the copy on a peer GPU.
-    `devices[0]` is the local GPU.  Uses mccs_hip_reduce_copy with the
-    register streaming loop (the access pattern of the ring's reduce-copy)."""
+    """Link bandwidth seen by this library's copy kernel: GB/s of bytes that
+    crossed a link (wall time over `reps` launches per job after a warm-up),
+    with one side of every copy in a peer GPU's HBM.  `devices[0]` is the
+    local GPU.  Uses mccs_hip_reduce_copy with the register streaming loop
+    (the access pattern of the ring's reduce-copy): a 1 -> k copy writes k
+    peers at once (push), a k -> 1 reduce reads k peers at once (pull), so
+    no device runs more than two launches at a time (a process's streams
+    share its 4 hardware queues; mccs_amd/_streams.py)."""
     import importlib
 
     R = importlib.import_module(__package__ + ".reduce")  # the module (the package exports a function `reduce`)
-
     devices = list(devices)
     nd = len(devices)
     distinct = len(set(devices)) == nd
@@ -146,16 +151,18 @@ def xgmi_calibration(torch, devices, nbytes: int = 64 << 20, reps: int = 10) -> 
 
     saved = R.get_tune()
 
-    def timed(jobs):
-        """jobs: list of (launching device index, dst tensor, src tensor); each
-        on its own stream of its launching device, all concurrently."""
-        streams = [torch.cuda.Stream(device=torch.device("cuda", devices[i])) for i, _, _ in jobs]
+    def timed(jobs, blocks_per_cu):
+        """jobs: (launching device index, dst list, src list, stream slot);
+        all concurrently.  Returns GB/s of link bytes: a job moves
+        max(len(dsts), len(srcs)) x nbytes across links."""
+        R.tune(1, 4, 1, blocks_per_cu, 0, 0)
+        streams = [side_stream(torch, devices[i], slot=10 + slot) for i, _, _, slot in jobs]
 
         def run(k):
-            for (i, dst, src), st in zip(jobs, streams):
+            for (i, dsts, srcs, _), st in zip(jobs, streams):
                 with torch.cuda.device(devices[i]):
                     for _ in range(k):
-                        R.reduce_copy([dst], [src], count=n, stream=st)
+                        R.reduce_copy(dsts, srcs, count=n, stream=st)
         run(1)
         for d in set(devices):
             torch.cuda.synchronize(d)
@@ -164,38 +171,48 @@ def xgmi_calibration(torch, devices, nbytes: int = 64 << 20, reps: int = 10) -> 
         for d in set(devices):
             torch.cuda.synchronize(d)
         el = time.perf_counter() - t0
-        return len(jobs) * reps * nbytes / el / 1e9
+        moved = sum(max(len(dsts), len(srcs)) for _, dsts, srcs, _ in jobs) * nbytes * reps
+        return moved / el / 1e9
 
-    out = {"bytes_per_copy": nbytes, "reps": reps, "kernel": "mccs_hip_reduce_copy 1->1 (REG loop, nt)",
-           "peers_distinct_gpus": distinct}
+    def groups(idx):  # at most 4 destinations per launch (MCCS_REDUCE_MAX_DSTS)
+        idx = list(idx)
+        return [idx[k:k + 4] for k in range(0, len(idx), 4)]
+
+    out = {"bytes_per_copy": nbytes, "reps": reps, "kernel": "mccs_hip_reduce_copy (REG loop, nt)",
+           "peers_distinct_gpus": distinct, "unit": "GB/s of bytes crossing links"}
     try:
         peers = range(1, nd)
-        # one link alone: full-grid copies
-        R.tune(1, 4, 1, 4, 0, 0)
         out["one_link"] = {
             "peer": devices[1],
-            "pull_GBps": round(timed([(0, buf(0, "dst"), buf(1, "src"))]), 2),
-            "push_GBps": round(timed([(0, buf(1, "dst"), buf(0, "src"))]), 2),
+            "pull_GBps": round(timed([(0, [buf(0, "dst")], [buf(1, "src")], 0)], 4), 2),
+            "push_GBps": round(timed([(0, [buf(1, "dst")], [buf(0, "src")], 0)], 4), 2),
+            # both directions of that link at once (each side pushes)
+            "bidirectional_push_GBps_total": round(
+                timed([(0, [buf(1, "dst")], [buf(0, "src")], 0), (1, [buf(0, "dst")], [buf(1, "src")], 0)], 4), 2),
         }
-        # both directions of that link at once (each side pushes)
-        R.tune(1, 4, 1, 2, 0, 0)
-        bi = timed([(0, buf(1, "dst"), buf(0, "src")), (1, buf(0, "dst"), buf(1, "src"))])
-        out["one_link"]["bidirectional_push_GBps_total"] = round(bi, 2)
         # every peer of device 0 alone, push and pull (link uniformity)
-        R.tune(1, 4, 1, 4, 0, 0)
-        out["per_peer"] = [{"peer": devices[q], "pull_GBps": round(timed([(0, buf(0, "dst"), buf(q, "src"))]), 2),
-                            "push_GBps": round(timed([(0, buf(q, "dst"), buf(0, "src"))]), 2)} for q in peers]
-        # every link of device 0 at once (one stream per peer, 1 block per CU each)
-        R.tune(1, 4, 1, 1, 0, 0)
+        out["per_peer"] = [{"peer": devices[q],
+                            "pull_GBps": round(timed([(0, [buf(0, "dst")], [buf(q, "src")], 0)], 4), 2),
+                            "push_GBps": round(timed([(0, [buf(q, "dst")], [buf(0, "src")], 0)], 4), 2)}
+                           for q in peers]
+        # every link of device 0 at once: one reduce reading all peers; pushes
+        # to all peers from a 1 -> 4 and a 1 -> 3 copy on two streams
+        pg = groups(peers)
         out["all_links_of_dev0"] = {
-            "pull_GBps_total": round(timed([(0, buf(0, f"dst{q}"), buf(q, "src")) for q in peers]), 2),
-            "push_GBps_total": round(timed([(0, buf(q, "dst0"), buf(0, "src")) for q in peers]), 2),
+            "pull_GBps_total": round(timed([(0, [buf(0, "dsum")], [buf(q, "src") for q in peers], 0)], 4), 2),
+            "push_GBps_total": round(timed([(0, [buf(q, "dst0") for q in g], [buf(0, "src")], k)
+                                            for k, g in enumerate(pg)], 4 // len(pg) or 1), 2),
         }
         # the ring's load: every device pushes to every peer at once
-        jobs = [(a, buf(b, f"dst{a}"), buf(a, "src")) for a in range(nd) for b in range(nd) if a != b]
-        tot = timed(jobs)
-        out["all_to_all_push"] = {"GBps_total": round(tot, 2), "directed_links": len(jobs),
-                                  "GBps_per_link_direction": round(tot / len(jobs), 2)}
+        jobs = []
+        for a in range(nd):
+            others = [b for b in range(nd) if b != a]
+            for k, g in enumerate(groups(others)):
+                jobs.append((a, [buf(b, f"dst{a}") for b in g], [buf(a, "src")], k))
+        tot = timed(jobs, max(1, 4 // max(1, len(groups(range(nd - 1))))))
+        links = nd * (nd - 1)
+        out["all_to_all_push"] = {"GBps_total": round(tot, 2), "directed_links": links,
+                                  "GBps_per_link_direction": round(tot / links, 2)}
         out["per_link_direction_GBps"] = out["all_to_all_push"]["GBps_per_link_direction"]
     except Exception as e:  # recorded, never fatal
         out["error"] = f"{type(e).__name__}: {e}"[:300]

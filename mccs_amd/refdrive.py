@@ -414,7 +414,9 @@ def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbyte
     send = exact_inputs(torch, count, rank, dtype, dev)
     want = expected_exact(torch, count, world, dtype, dev)
     recv = torch.empty_like(send)
-    stream = torch.cuda.Stream(device=dev)
+    from ._streams import side_stream
+
+    stream = side_stream(torch, device, slot=2)
 
     def allgather(obj):
         out = [None] * world

@@ -257,8 +257,10 @@ def shared_gpu_lanes(world: int) -> int:
 def graph_replay(torch, dist, comm, call_on, calls=10):
     """Per-call time of `calls` AllReduces captured in one HIP graph (max over
     ranks), after one untimed replay.  call_on(stream) issues one AllReduce."""
+    from ._streams import side_stream
+
     torch.cuda.synchronize()
-    gs = torch.cuda.Stream()
+    gs = side_stream(torch, slot=1)  # one graph stream per process (mccs_amd/_streams.py)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=gs):
         for _ in range(calls):
@@ -734,7 +736,9 @@ def setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup
                                      modes, (count, torch.float16, C.AllReduceDataType.Float16), grp)
     if comm is None:
         raise BenchFailure(f"{name}: communicator creation failed")
-    stream = torch.cuda.Stream(dev)
+    from ._streams import side_stream
+
+    stream = side_stream(torch, device, slot=2)
     tj = traffic.TraceJob(torch, name, [comm], [jrank], half, count, compute_us * 1e-6 * compute_scale, stream, dev)
     dist.barrier()  # both jobs start together
     for w in range(warmup):

@@ -32,5 +32,6 @@ def test_xgmi_calibration_code_path():
     assert r["peers_distinct_gpus"] is False
     assert r["one_link"]["pull_GBps"] > 0 and r["one_link"]["push_GBps"] > 0
     assert len(r["per_peer"]) == 2 and r["all_to_all_push"]["directed_links"] == 6
+    assert r["all_links_of_dev0"]["pull_GBps_total"] > 0 and r["all_links_of_dev0"]["push_GBps_total"] > 0
     assert r["per_link_direction_GBps"] > 0
     assert R.get_tune() == before  # the reduce tuning is restored
