@@ -156,7 +156,7 @@ def xgmi_calibration(torch, devices, nbytes: int = 64 << 20, reps: int = 10) -> 
         all concurrently.  Returns GB/s of link bytes: a job moves
         max(len(dsts), len(srcs)) x nbytes across links."""
         R.tune(1, 4, 1, blocks_per_cu, 0, 0)
-        streams = [side_stream(torch, devices[i], slot=10 + slot) for i, _, _, slot in jobs]
+        streams = [side_stream(torch, devices[i], slot=slot) for i, _, _, slot in jobs]  # the legs' streams, reused
 
         def run(k):
             for (i, dsts, srcs, _), st in zip(jobs, streams):

@@ -416,7 +416,7 @@ def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbyte
     recv = torch.empty_like(send)
     from ._streams import side_stream
 
-    stream = side_stream(torch, device, slot=2)
+    stream = side_stream(torch, device, slot=1)
 
     def allgather(obj):
         out = [None] * world

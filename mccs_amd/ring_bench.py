@@ -738,7 +738,7 @@ def setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup
         raise BenchFailure(f"{name}: communicator creation failed")
     from ._streams import side_stream
 
-    stream = side_stream(torch, device, slot=2)
+    stream = side_stream(torch, device, slot=1)
     tj = traffic.TraceJob(torch, name, [comm], [jrank], half, count, compute_us * 1e-6 * compute_scale, stream, dev)
     dist.barrier()  # both jobs start together
     for w in range(warmup):
