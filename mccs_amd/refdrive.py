@@ -272,7 +272,9 @@ class RefDrivenRank:
 
     def all_reduce(self, send_ptr: int, recv_ptr: int, count: int, dtype: int, op: int, stream: int) -> None:
         """One AllReduce task through plan.rs's path (one work element per
-        selected channel), launched on `stream`."""
+        selected channel), launched on `stream`.  count = 0 launches nothing."""
+        if count == 0:
+            return
         nbytes = count * ESIZE[dtype]
         sch, nthr = ctypes.c_int(), ctypes.c_int()
         self.lib.mccs_task_schema(nbytes, self.nch, ctypes.byref(sch), ctypes.byref(nthr))
