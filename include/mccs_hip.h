@@ -112,8 +112,8 @@ typedef struct mccsComm *mccsComm_t;
 
 /* Communicator profile: comm_default_config (mccs.toml:18-20, config.rs:15-97)
  * plus the MI355X execution knobs.  Zero fields take defaults.
- * ABI note: `fifo_slots` was appended in library version 0.3, which grew the
- * struct; mccsCommConfigDefault() writes sizeof(mccsCommConfig) bytes, so a
+ * ABI note: `fifo_slots` and `direct_bytes` were appended in library version
+ * 0.3, which grew the struct; mccsCommConfigDefault() writes sizeof(mccsCommConfig) bytes, so a
  * caller compiled against an older header must be rebuilt.  Callers binding
  * the struct by hand (ctypes, bindgen) check mccsCommConfigSize(). */
 typedef struct {
@@ -131,6 +131,12 @@ typedef struct {
                            MCCS_BUFFER_SLOTS), 16 or 32; 0 = default (16).  More slots = more slices in
                            flight per lane; the chunk schedule (and so every result) still follows
                            buffer_size, as in the reference */
+  int direct_bytes;     /* AllReduce buckets of at most this many bytes per rank run the direct
+                           (two-shot) kernel on a fully connected node of <= 8 ranks: every chunk to
+                           its ring owner, reduced in the ring's order, results broadcast, so the
+                           output equals the ring's bit for bit; larger buckets take the ring.
+                           0 = default (MCCS_DIRECT_BYTES), < 0 = never.  Every rank must agree
+                           (it sizes the arena: Connect refuses a mismatch) */
 } mccsCommConfig;
 
 void mccsCommConfigDefault(mccsCommConfig *cfg);
@@ -176,6 +182,11 @@ mccsResult_t mccsCommDestroy(mccsComm_t comm);
 mccsResult_t mccsCommInfo(mccsComm_t comm, int *info7);
 /* ring send order of channel ch (nranks ints). */
 mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int *order);
+/* Algorithm of the comm's latest launch: MCCS_ALGO_RING or MCCS_ALGO_DIRECT
+ * (-1 before the first). */
+#define MCCS_ALGO_RING 0
+#define MCCS_ALGO_DIRECT 1
+int mccsCommLastAlgo(mccsComm_t comm);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
 const char *mccsGetErrorString(mccsResult_t r);

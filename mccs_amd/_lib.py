@@ -70,7 +70,7 @@ class _CommConfig(ctypes.Structure):
     _fields_ = [("channel_count", _c_int), ("buffer_size", _c_int), ("lanes", _c_int),
                 ("block_threads", _c_int), ("locality", _c_int), ("fifo_memory", _c_int),
                 ("timeout_ms", _c_int), ("work_fifo_depth", _c_int), ("bridge_streams", _c_int),
-                ("rings", _P(_c_int)), ("fifo_slots", _c_int)]
+                ("rings", _P(_c_int)), ("fifo_slots", _c_int), ("direct_bytes", _c_int)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/mccs_hip.h
@@ -105,6 +105,7 @@ SIGNATURES: dict[str, tuple] = {
     "mccsCommInfo": (_c_int, [_c_void_p, _P(_c_int)]),
     "mccsCommRing": (_c_int, [_c_void_p, _c_int, _P(_c_int)]),
     "mccsCommDevComm": (_c_int, [_c_void_p, _P(_c_void_p)]),
+    "mccsCommLastAlgo": (_c_int, [_c_void_p]),
     "mccs_ring_profile": (_c_int, [_c_int, _P(ctypes.c_ulonglong), _c_int]),
     "mccsMemAllocShared": (_c_int, [_c_int, _c_size_t, _P(_c_void_p), _c_void_p]),
     "mccsMemFreeShared": (_c_int, [_c_int, _c_void_p]),
@@ -144,7 +145,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mccsCommConfigSize() != ctypes.sizeof(_CommConfig):  # the struct grew once (mccs_hip.h ABI note)
+    if lib.mccsCommConfigSize() != ctypes.sizeof(_CommConfig):  # the struct grew in 0.3 (mccs_hip.h ABI note)
         raise RuntimeError(f"{p}: mccsCommConfig is {lib.mccsCommConfigSize()} bytes, this binding "
                            f"{ctypes.sizeof(_CommConfig)}: rebuild or update mccs_amd/_lib.py")
     _lib = lib

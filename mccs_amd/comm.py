@@ -81,6 +81,7 @@ class CommConfig:
     bridge_streams: int | None = None
     rings: list | None = None  # comm_patterns_override: channel_count x nranks send orders
     fifo_slots: int | None = None  # FIFO slots per connection: 8 (reference), 16, 32
+    direct_bytes: int | None = None  # largest bucket (bytes per rank) for the direct two-shot kernel; < 0 never
 
     def to_c(self, nranks: int):
         c = _CommConfig()
@@ -142,6 +143,11 @@ class Communicator:
             _lib.check(_sig().mccsCommRing(self._h, ch, arr), "mccsCommRing")
             out.append(list(arr))
         return out
+
+    def last_algo(self) -> str | None:
+        """"ring" or "direct": the algorithm of the latest launch (None before one)."""
+        a = _sig().mccsCommLastAlgo(self._h)
+        return {0: "ring", 1: "direct"}.get(a)
 
     def dev_comm(self) -> int:
         p = ctypes.c_void_p()

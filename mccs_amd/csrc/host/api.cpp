@@ -27,13 +27,14 @@ static thread_local GroupState g_group;
 
 // Drops every plan queued in the current group (error path).
 static void group_discard() {
-  for (Comm* c : g_group.comms) {
-    for (auto& s : c->sched) s = ChannelSchedule{};
-    c->plan_pending = false;
-  }
+  for (Comm* c : g_group.comms) plan_discard(c);
   g_group.comms.clear();
   g_group.streams.clear();
 }
+
+// Direct AllReduce threshold when the config leaves it 0 (MCCS_DIRECT_BYTES
+// overrides): buckets up to this many bytes per rank take the two-shot kernel.
+static constexpr int kDirectDefaultBytes = 0;
 
 static void fill_defaults(mccsCommConfig* c) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
@@ -48,6 +49,7 @@ static void fill_defaults(mccsCommConfig* c) {
   // bytes in flight per lane to cover an xGMI hop; 2 x the FIFO memory
   // (8 MiB per connection)
   if (c->fifo_slots == 0) c->fifo_slots = 2 * MCCS_BUFFER_SLOTS;
+  if (c->direct_bytes == 0) c->direct_bytes = kDirectDefaultBytes;
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
@@ -67,6 +69,7 @@ static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
     return mccsInvalidArgument;
   if (nranks < 1 || nranks > 64) return mccsInvalidArgument;
   if (c.fifo_slots != 8 && c.fifo_slots != 16 && c.fifo_slots != 32) return mccsInvalidArgument;
+  if (c.direct_bytes > (1 << 30)) return mccsInvalidArgument;  // 9 slots of it live in every rank's arena
   return mccsSuccess;
 }
 
@@ -184,7 +187,8 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   cfg->bridge_streams = -1;
   // operator overrides (no rebuild needed): MCCS_LOCALITY=sender|receiver,
   // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE,
-  // MCCS_BRIDGE_STREAMS, MCCS_FIFO_MEMORY=uncached|device, MCCS_FIFO_SLOTS
+  // MCCS_BRIDGE_STREAMS, MCCS_FIFO_MEMORY=uncached|release|device,
+  // MCCS_FIFO_SLOTS, MCCS_DIRECT_BYTES
   if (const char* v = std::getenv("MCCS_LOCALITY"))
     cfg->locality = (v[0] == 's' || v[0] == 'S') ? MCCS_LOCALITY_SENDER : MCCS_LOCALITY_RECEIVER;
   if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
@@ -197,6 +201,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   if (const char* v = std::getenv("MCCS_CHANNELS")) cfg->channel_count = std::atoi(v);
   if (const char* v = std::getenv("MCCS_BUFFER_SIZE")) cfg->buffer_size = std::atoi(v);
   if (const char* v = std::getenv("MCCS_FIFO_SLOTS")) cfg->fifo_slots = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_DIRECT_BYTES")) cfg->direct_bytes = std::atoi(v);
 }
 
 extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {
@@ -210,6 +215,7 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
     Comm* c = cs[i];
     int share = 0;
     for (int j = 0; j < nranks; ++j) share += devices[j] == devices[i];
+    c->share = share;
     if (share < 2 || c->cfg.lanes > 0) continue;
     const int cap = coresident_ring_blocks(c->block_threads, c->device);
     const int fit = cap / (share * c->nch);
@@ -324,6 +330,7 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
       max_share = std::max(max_share, share);
       if (hs[r].ring_cap > 0) cap = std::min(cap, (int)hs[r].ring_cap);
     }
+    c->share = max_share;
     if (max_share > 1 && cap < (1 << 30)) {
       if (hs[0].lanes_auto) {
         const int fit = cap / 2 / (max_share * c->nch);
@@ -440,6 +447,11 @@ extern "C" mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int* order) {
   if (!c || !order || ch < 0 || ch >= c->nch) return mccsInvalidArgument;
   for (int i = 0; i < c->nranks; ++i) order[i] = c->rings[ch][i];
   return mccsSuccess;
+}
+
+extern "C" int mccsCommLastAlgo(mccsComm_t comm) {
+  const Comm* c = (const Comm*)comm;
+  return c ? c->last_algo : -1;
 }
 
 extern "C" mccsResult_t mccsCommDevComm(mccsComm_t comm, void** dev_comm) {

@@ -59,17 +59,24 @@ struct DeviceGuard {
 
 // Per-rank FIFO arena layout (identical on every rank; offsets in bytes).
 // [flags: nch x {send head lines, recv tail lines}] [data: nch x fifo_bytes]
+// [direct region (64 KiB aligned), when direct_slot > 0: control + in/out
+//  slots of the direct AllReduce, ring_cfg.h]
 // fifo_bytes = fifo_slots x buffer_size / 8 (slots of the reference step size)
 struct ArenaLayout {
   int nch = 0;
   size_t buffer_size = 0;
   size_t fifo_bytes = 0;
+  size_t direct_slot = 0;  // bytes of one direct in/out slot (0: no direct region)
   static constexpr size_t kLinesBytes = (size_t)MCCS_MAX_LANES * MCCS_FLAG_LINE_BYTES;  // 8 KiB
   size_t head_off(int c) const { return (size_t)c * 2 * kLinesBytes; }
   size_t tail_off(int c) const { return (size_t)c * 2 * kLinesBytes + kLinesBytes; }
   size_t flags_bytes() const { return (((size_t)nch * 2 * kLinesBytes) + 65535) & ~(size_t)65535; }
   size_t data_off(int c) const { return flags_bytes() + (size_t)c * fifo_bytes; }
-  size_t total() const { return flags_bytes() + (size_t)nch * fifo_bytes; }
+  size_t ring_total() const { return flags_bytes() + (size_t)nch * fifo_bytes; }
+  size_t direct_off() const { return (ring_total() + 65535) & ~(size_t)65535; }
+  size_t total() const {
+    return direct_slot ? direct_off() + MCCS_DIRECT_CTRL_BYTES + (size_t)MCCS_DIRECT_SLOTS * direct_slot : ring_total();
+  }
 };
 
 // Connect handle exchanged between processes (fixed size, POD).
@@ -163,6 +170,16 @@ struct Comm {
   std::vector<ChannelSchedule> sched;
   int plan_func = -1, plan_dtype = -1, plan_op = -1, plan_threads = 0;
   bool plan_pending = false;
+  // direct AllReduce (direct_kernel.h): the pending call when the plan is one
+  // AllReduce of at most layout.direct_slot bytes (plan.cpp)
+  bool plan_direct = false;
+  struct {
+    const void* send;
+    void* recv;
+    size_t count;
+  } direct{};
+  int share = 1;         // ranks of this communicator on this rank's GPU (co-residency of spinning launches)
+  int last_algo = -1;    // MCCS_ALGO_* of the latest launch
 };
 
 // comm.cpp
@@ -177,12 +194,15 @@ mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm even
 int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live library comm's device struct, else 0
 void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
 // plan.cpp
+void plan_discard(Comm* c);  // drops the pending plan
 mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count);
 mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams);
 // ring.hip
 const void* ring_kernel_ptr(int func, int dtype, int op);
 const void* ring_multi_kernel_ptr(int func, int dtype, int op);
 int coresident_ring_blocks(int block, int device);
+// direct.hip
+const void* direct_kernel_ptr(int dtype, int op);
 hipError_t ring_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_flush_caches(hipStream_t st);
 

@@ -71,9 +71,7 @@ static void enqueue_elem(ChannelSchedule& s, const WorkElemHost& e, int func_ind
   s.work_func.push_back(func_index);
 }
 
-mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count) {
-  if (c->plan_pending && (c->plan_func != func || c->plan_dtype != dtype || c->plan_op != op))
-    return mccsInvalidUsage;  // pre_launch_schedule batches same func/dtype/op only (plan.rs:122-141)
+static mccsResult_t ring_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count) {
   const size_t esize = (size_t)elem_bytes(dtype);
   const size_t total = func == mccsFuncAllGather ? count * c->nranks : count * esize;  // task.rs:95-102
   int nch = 0, nthr = 0;
@@ -95,6 +93,43 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   c->plan_dtype = dtype;
   c->plan_op = op;
   return mccsSuccess;
+}
+
+void plan_discard(Comm* c) {
+  for (auto& s : c->sched) s = ChannelSchedule{};
+  c->plan_pending = false;
+  c->plan_direct = false;
+}
+
+// A pending direct AllReduce goes back to the ring after all: the group holds
+// another collective of this comm, or the device's fused launch cannot run it.
+static mccsResult_t demote_direct(Comm* c) {
+  if (!c->plan_direct) return mccsSuccess;
+  c->plan_direct = false;
+  c->plan_pending = false;
+  return ring_enqueue(c, c->plan_func, c->plan_dtype, c->plan_op, c->direct.send, c->direct.recv, c->direct.count);
+}
+
+mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count) {
+  if (c->plan_pending && (c->plan_func != func || c->plan_dtype != dtype || c->plan_op != op))
+    return mccsInvalidUsage;  // pre_launch_schedule batches same func/dtype/op only (plan.rs:122-141)
+  MCCS_CHECK(demote_direct(c));
+  // One AllReduce that fits the direct region (every rank decides alike: same
+  // call, same config) is held for the direct kernel; the launch may still
+  // send it to the ring (plan_launch_group).
+  if (!c->plan_pending && func == mccsFuncAllReduce && c->layout.direct_slot > 0 &&
+      count * (size_t)elem_bytes(dtype) <= (size_t)c->cfg.direct_bytes) {
+    c->plan_direct = true;
+    c->direct.send = send;
+    c->direct.recv = recv;
+    c->direct.count = count;
+    c->plan_pending = true;
+    c->plan_func = func;
+    c->plan_dtype = dtype;
+    c->plan_op = op;
+    return mccsSuccess;
+  }
+  return ring_enqueue(c, func, dtype, op, send, recv, count);
 }
 
 static mccsDevWork to_dev_work(const std::vector<WorkElemHost>& elems, bool in_fifo, bool is_last, uint32_t u) {
@@ -332,13 +367,154 @@ int coresident_ring_blocks(int block, int device) {
   return cache[{device, block}] = best * ncu;
 }
 
+// Workgroups of the direct kernels the device holds at once (min over the
+// instantiations): a direct launch spins on peers' flags, so all of its
+// workgroups, and those of ranks sharing the GPU, must be resident together.
+static int coresident_direct_blocks(int device) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(device);
+    if (it != cache.end()) return it->second;
+  }
+  DeviceGuard g(device);
+  int ncu = 0;
+  if (rt().CuCount(&ncu, device) != hipSuccess) return 0;
+  int best = 1 << 30;
+  for (int dt = 0; dt < mccsNumTypes; ++dt)
+    for (int op = 0; op < 4; ++op) {
+      int per_cu = 0;
+      const void* fn = direct_kernel_ptr(dt, op);
+      if (!fn || rt().BlocksPerCu(&per_cu, fn, MCCS_DIRECT_THREADS) != hipSuccess) per_cu = 0;
+      best = std::min(best, per_cu);
+    }
+  std::lock_guard<std::mutex> lk(mu);
+  return cache[device] = best * ncu;
+}
+
+// Sub-tiles the direct kernel deals to its workgroups (direct_kernel.h
+// direct_items, the ring's chunk walk cut into 64 KiB pieces).
+static uint32_t direct_item_count(size_t count, size_t esize, int n, int nch, int nthr, int buff) {
+  const int64_t size = (int64_t)count;
+  const int64_t chunk = (int64_t)(buff / MCCS_BUFFER_SLOTS / (int)esize) * ALLREDUCE_CHUNKSTEPS;
+  const int64_t loop = (int64_t)nch * n * chunk;
+  int64_t gran = (int64_t)(nthr - WARP_SIZE) * 8 / (int64_t)esize;
+  if (gran < 1) gran = 1;
+  const int64_t sub = 65536 / (int64_t)esize;
+  uint64_t items = 0;
+  for (int64_t g = 0; g < size; g += loop) {
+    int64_t rcs = (size - g + (int64_t)nch * n - 1) / ((int64_t)nch * n);
+    rcs = std::min(chunk, rcs);
+    rcs = (rcs + gran - 1) / gran * gran;
+    for (int64_t c = 0; c < (int64_t)nch * n; ++c) {
+      const int64_t ne = std::min(rcs, size - (g + c * rcs));
+      if (ne > 0) items += (uint64_t)((ne + sub - 1) / sub);
+    }
+  }
+  return (uint32_t)std::min<uint64_t>(items, 1u << 30);
+}
+
+// MCCS_DIRECT_BLOCKS: most workgroups per rank of a direct launch (default 128).
+static int direct_max_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("MCCS_DIRECT_BLOCKS");
+    const int x = e ? std::atoi(e) : 0;
+    return x > 0 ? x : 128;
+  }();
+  return v;
+}
+
+// Every comm of the device group holds one direct AllReduce of the same shape
+// (fused ranks share the launch's walk arguments).
+static bool direct_group(std::vector<Comm*>& comms, const std::vector<int>& idx) {
+  const Comm* c0 = comms[idx[0]];
+  for (size_t k = 0; k < idx.size(); ++k) {
+    const Comm* ck = comms[idx[k]];
+    if (!ck->plan_direct) return false;
+    if (ck->nranks != c0->nranks || ck->direct.count != c0->direct.count || ck->plan_dtype != c0->plan_dtype ||
+        ck->plan_op != c0->plan_op || ck->rings != c0->rings || ck->cfg.buffer_size != c0->cfg.buffer_size ||
+        ck->layout.direct_slot != c0->layout.direct_slot || ck->nch != c0->nch)
+      return false;
+  }
+  return idx.size() <= MCCS_MULTI_MAX_RANKS;
+}
+
+// The direct launch's arguments: the ring walk this call would take (the
+// channels and thread count of get_task_schema, each channel's ring read as
+// rank-at-ring-index, engine.rs:274-286) and every rank slot's buffers and
+// direct regions.
+static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<int>& idx, mccsDirectArgs* da,
+                                 unsigned* grid_x) {
+  const Comm* c0 = comms[idx[0]];
+  const size_t esize = (size_t)elem_bytes(c0->plan_dtype);
+  int nch = 0, nthr = 0;
+  task_schema(c0->direct.count * esize, c0->nch, &nch, &nthr);
+  const std::vector<int> chans = select_channels(c0, nch);
+  std::memset(da, 0, sizeof(*da));
+  const int n = c0->nranks;
+  da->count = c0->direct.count;
+  da->slot_bytes = c0->layout.direct_slot;
+  da->nranks = (uint32_t)n;
+  da->nch = (uint32_t)chans.size();
+  da->nthr_ref = (uint32_t)nthr;
+  da->buff_size = (uint32_t)c0->cfg.buffer_size;
+  da->fence_mode = c0->kcfg.fence_mode;
+  da->timeout_ticks = c0->kcfg.timeout_ticks;
+  for (size_t bid = 0; bid < chans.size(); ++bid) {
+    const std::vector<int>& ring = c0->rings[chans[bid]];
+    const int pos0 = (int)(std::find(ring.begin(), ring.end(), 0) - ring.begin());
+    for (int k = 0; k < n; ++k) da->idx2rank[bid][k] = (uint8_t)ring[(pos0 + k) % n];
+  }
+  for (size_t k = 0; k < idx.size(); ++k) {
+    const Comm* ck = comms[idx[k]];
+    mccsDirectRank& r = da->r[k];
+    r.send = ck->direct.send;
+    r.recv = ck->direct.recv;
+    for (int t = 0; t < n; ++t) {
+      if (!ck->peer_arena[t]) return mccsInternalError;
+      r.region[t] = ck->peer_arena[t] + ck->layout.direct_off();
+    }
+    r.comm = (mccsDevComm*)ck->d_comm;
+    r.rank = (uint32_t)ck->rank;
+    r.err_line = 1;
+    // safest hand-off of the group, as for the ring (SYSTEM > UNCACHED_RELEASE > UNCACHED)
+    if (ck->kcfg.fence_mode == MCCS_FENCE_SYSTEM) da->fence_mode = MCCS_FENCE_SYSTEM;
+    else if (ck->kcfg.fence_mode == MCCS_FENCE_UNCACHED_RELEASE && da->fence_mode == MCCS_FENCE_UNCACHED)
+      da->fence_mode = MCCS_FENCE_UNCACHED_RELEASE;
+    da->timeout_ticks = (da->timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)
+                            ? 0
+                            : std::max(da->timeout_ticks, ck->kcfg.timeout_ticks);
+  }
+  const int cap = coresident_direct_blocks(c0->device);
+  long g = std::min<long>(direct_item_count(da->count, esize, n, (int)da->nch, nthr, (int)da->buff_size),
+                          direct_max_blocks());
+  if (idx.size() > 1) g = std::min<long>(g, cap / (long)idx.size());  // one fused launch: co-scheduled
+  else if (c0->share > 1) g = std::min<long>(g, cap / 2 / c0->share);  // separate processes: half the slots
+  g = std::max<long>(g, 1);
+  if (g * (long)idx.size() > cap) {
+    MCCS_LOG("direct launch of %zu ranks x %ld workgroups exceeds the %d co-resident ones of device %d", idx.size(),
+             g, cap, c0->device);
+    return mccsInvalidUsage;
+  }
+  *grid_x = (unsigned)g;
+  for (size_t k = 0; k < idx.size(); ++k) {
+    Comm* ck = comms[idx[k]];
+    ck->plan_direct = false;
+    ck->plan_pending = false;
+  }
+  return mccsSuccess;
+}
+
 // Launch every pending plan.  By default a comm launches on the caller's
 // stream (stream order equals libmccs's bridge).  With bridge_streams = 1 it
 // launches on its own stream, bridged to the caller's with events like
 // libmccs (collectives.rs:86,134 + proxy/engine.rs:1185-1189).  Comms sharing
-// a device are fused into one multi-rank launch so their ring blocks are
+// a device are fused into one multi-rank launch so their blocks are
 // co-resident (they spin on each other's flags); events join their streams
-// only when the callers used different ones.
+// only when the callers used different ones.  A device group whose comms each
+// hold one direct-sized AllReduce runs the direct kernel, anything else the
+// ring.
 mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams) {
   std::map<int, std::vector<int>> by_dev;
   for (int i = 0; i < (int)comms.size(); ++i)
@@ -346,7 +522,10 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
   for (auto& kv : by_dev) {
     const std::vector<int>& idx = kv.second;
     DeviceGuard g(kv.first);
-    if (idx.size() > 1) {  // checked before any work is uploaded, so the comms stay usable
+    const bool direct = direct_group(comms, idx);
+    if (!direct)
+      for (int i : idx) MCCS_CHECK(demote_direct(comms[i]));
+    if (!direct && idx.size() > 1) {  // checked before any work is uploaded, so the comms stay usable
       const Comm* c0 = comms[idx[0]];
       const int cap = coresident_ring_blocks(c0->block_threads, kv.first);
       const long need = (long)c0->nch * c0->lanes * (long)idx.size();
@@ -362,17 +541,59 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     MCCS_HIP(rt().StreamIsCapturing(user_streams[idx[0]], &capturing));
     std::vector<LaunchDesc> lds(idx.size());
     mccsMultiLaunchArgs ma;
-    std::memset(&ma, 0, sizeof(ma));
-    int per_rank = inline_channels(comms[idx[0]]);
-    for (size_t k = 1; k < idx.size() && per_rank > 0; ++k)
-      if (inline_channels(comms[idx[k]]) != per_rank) per_rank = 0;
-    if (per_rank > 0 && per_rank * idx.size() <= MCCS_INLINE_WORKS) {
-      for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work_inline(comms[idx[k]], &lds[k], &ma));
-    } else {
-      for (size_t k = 0; k < idx.size(); ++k)
-        MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k]) : upload_work(comms[idx[k]], &lds[k]));
-    }
+    mccsDirectArgs da;
+    const void* fn = nullptr;
+    void* args[1] = {nullptr};
+    unsigned grid = 0, block = 0;
+    bool work_inline = true;  // no work-FIFO entries to acknowledge
     Comm* c0 = comms[idx[0]];
+    if (direct) {
+      MCCS_CHECK(build_direct(comms, idx, &da, &grid));
+      fn = direct_kernel_ptr(c0->plan_dtype, c0->plan_op);
+      if (!fn) return mccsInvalidArgument;
+      block = MCCS_DIRECT_THREADS;
+      args[0] = &da;
+    } else {
+      std::memset(&ma, 0, sizeof(ma));
+      int per_rank = inline_channels(comms[idx[0]]);
+      for (size_t k = 1; k < idx.size() && per_rank > 0; ++k)
+        if (inline_channels(comms[idx[k]]) != per_rank) per_rank = 0;
+      if (per_rank > 0 && per_rank * idx.size() <= MCCS_INLINE_WORKS) {
+        for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work_inline(comms[idx[k]], &lds[k], &ma));
+      } else {
+        for (size_t k = 0; k < idx.size(); ++k)
+          MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k]) : upload_work(comms[idx[k]], &lds[k]));
+      }
+      // Communicator launches carry their hand-off policy in the arguments
+      // (one launch per device; blockIdx.y = rank slot when ranks share it).
+      // Fused ranks take the safest policy of the group.
+      if (idx.size() > MCCS_MULTI_MAX_RANKS) return mccsInvalidUsage;
+      ma.channelMask = lds[0].mask;
+      ma.cfg = c0->kcfg;
+      for (size_t k = 0; k < idx.size(); ++k) {
+        const Comm* ck = comms[idx[k]];
+        if (lds[k].mask != lds[0].mask || lds[k].multi_fn != lds[0].multi_fn || ck->lanes != c0->lanes ||
+            ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps ||
+            ck->kcfg.fifo_slots != c0->kcfg.fifo_slots)
+          return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
+        ma.comm[k] = (mccsDevComm*)ck->d_comm;
+        ma.work[k] = lds[k].work;
+        ma.view[k] = ck->d_view;
+        // safest of the group: SYSTEM > UNCACHED_RELEASE > UNCACHED
+        if (ck->kcfg.fence_mode == MCCS_FENCE_SYSTEM) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
+        else if (ck->kcfg.fence_mode == MCCS_FENCE_UNCACHED_RELEASE && ma.cfg.fence_mode == MCCS_FENCE_UNCACHED)
+          ma.cfg.fence_mode = MCCS_FENCE_UNCACHED_RELEASE;
+        ma.cfg.timeout_ticks = (ma.cfg.timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)
+                                   ? 0
+                                   : std::max(ma.cfg.timeout_ticks, ck->kcfg.timeout_ticks);
+        ma.cfg.profile |= ck->kcfg.profile;
+      }
+      fn = lds[0].multi_fn;
+      grid = (unsigned)(lds[0].nch_used * c0->lanes);
+      block = (unsigned)c0->block_threads;
+      args[0] = &ma;
+      work_inline = lds[0].work_inline;
+    }
     const bool bridge = c0->cfg.bridge_streams >= 0;
     hipStream_t st = user_streams[idx[0]];
     if (bridge) MCCS_CHECK(comm_stream(c0, &st));
@@ -386,33 +607,6 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
         MCCS_HIP(rt().StreamWaitEvent(st, c->user_event));
       }
     }
-    const unsigned grid = (unsigned)(lds[0].nch_used * c0->lanes);
-    const unsigned block = (unsigned)c0->block_threads;
-    // Communicator launches carry their hand-off policy in the arguments
-    // (one launch per device; blockIdx.y = rank slot when ranks share it).
-    // Fused ranks take the safest policy of the group.
-    if (idx.size() > MCCS_MULTI_MAX_RANKS) return mccsInvalidUsage;
-    ma.channelMask = lds[0].mask;
-    ma.cfg = c0->kcfg;
-    for (size_t k = 0; k < idx.size(); ++k) {
-      const Comm* ck = comms[idx[k]];
-      if (lds[k].mask != lds[0].mask || lds[k].multi_fn != lds[0].multi_fn || ck->lanes != c0->lanes ||
-          ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps ||
-          ck->kcfg.fifo_slots != c0->kcfg.fifo_slots)
-        return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
-      ma.comm[k] = (mccsDevComm*)ck->d_comm;
-      ma.work[k] = lds[k].work;
-      ma.view[k] = ck->d_view;
-      // safest of the group: SYSTEM > UNCACHED_RELEASE > UNCACHED
-      if (ck->kcfg.fence_mode == MCCS_FENCE_SYSTEM) ma.cfg.fence_mode = MCCS_FENCE_SYSTEM;
-      else if (ck->kcfg.fence_mode == MCCS_FENCE_UNCACHED_RELEASE && ma.cfg.fence_mode == MCCS_FENCE_UNCACHED)
-        ma.cfg.fence_mode = MCCS_FENCE_UNCACHED_RELEASE;
-      ma.cfg.timeout_ticks = (ma.cfg.timeout_ticks == 0 || ck->kcfg.timeout_ticks == 0)
-                                 ? 0
-                                 : std::max(ma.cfg.timeout_ticks, ck->kcfg.timeout_ticks);
-      ma.cfg.profile |= ck->kcfg.profile;
-    }
-    void* args[1] = {&ma};
     // The launching comm's event rides on the dispatch's own completion signal
     // (hipExtLaunchKernel stopEvent): a hipEventRecord behind the kernel is a
     // marker packet that cost ~3 us of device time per launch on MI355X, the
@@ -421,12 +615,12 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     // (exported to a backend: recorded the usual way).
     const bool stop_on_launch = !capturing && !c0->event_ipc;
     const dim3 g3(grid, (unsigned)idx.size());
-    if (stop_on_launch) MCCS_HIP(rt().LaunchKernelExt(lds[0].multi_fn, g3, dim3(block), args, st, c0->event));
-    else MCCS_HIP(rt().LaunchKernel(lds[0].multi_fn, g3, dim3(block), args, st));
+    if (stop_on_launch) MCCS_HIP(rt().LaunchKernelExt(fn, g3, dim3(block), args, st, c0->event));
+    else MCCS_HIP(rt().LaunchKernel(fn, g3, dim3(block), args, st));
     // Other events are recorded only when consumed (Comm::event_recorded):
     // cross-stream ordering, an exported backend event, or a work-FIFO launch
     // (wait_work_queue queries the event to tell a stuck kernel from a slow one).
-    bool record = events || !lds[0].work_inline || eager_events();
+    bool record = events || !work_inline || eager_events();
     for (size_t k = 0; k < idx.size() && !record; ++k) record = comms[idx[k]]->event_ipc;
     if (record && !stop_on_launch) MCCS_HIP(rt().EventRecord(c0->event, st));
     if (events) {
@@ -437,7 +631,10 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     }
     if (record)
       for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
-    for (size_t k = 0; k < idx.size(); ++k) comms[idx[k]]->event_recorded = record;
+    for (size_t k = 0; k < idx.size(); ++k) {
+      comms[idx[k]]->event_recorded = record;
+      comms[idx[k]]->last_algo = direct ? MCCS_ALGO_DIRECT : MCCS_ALGO_RING;
+    }
     c0->event_recorded = record || stop_on_launch;
   }
   return mccsSuccess;

@@ -217,14 +217,26 @@ class FakeRuntime final : public DeviceRuntime {
     // every communicator of a fused ring launch must live on the launching device
     bool on_dev = true;
     unsigned inl = 0;
+    std::string extra;
+    bool direct = false;
+    for (int dt = 0; dt < mccsNumTypes && fn; ++dt)
+      for (int op = 0; op < 4; ++op) direct = direct || fn == direct_kernel_ptr(dt, op);
     if (fn && args && grid.y >= 1 && grid.y <= MCCS_MULTI_MAX_RANKS) {
-      const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
-      for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(ma->comm[k]) == cur_;
-      inl = ma->inline_works;
+      if (direct) {  // mccsDirectArgs: the walk it reproduces
+        const mccsDirectArgs* da = (const mccsDirectArgs*)args[0];
+        for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(da->r[k].comm) == cur_;
+        extra = " count=" + std::to_string(da->count) + " nch=" + std::to_string(da->nch) +
+                " nthr=" + std::to_string(da->nthr_ref) + " fence=" + std::to_string(da->fence_mode);
+      } else {
+        const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
+        for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(ma->comm[k]) == cur_;
+        inl = ma->inline_works;
+      }
     }
     note("launch dev=" + std::to_string(cur_) + " grid=" + std::to_string(grid.x) + "x" + std::to_string(grid.y) +
          " block=" + std::to_string(block.x) + " stream=" + sid(s) + " comms_on_dev=" + (on_dev ? "1" : "0") +
-         " inline_works=" + std::to_string(inl) + " stop_event=" + std::to_string((uintptr_t)stop_));
+         " inline_works=" + std::to_string(inl) + " stop_event=" + std::to_string((uintptr_t)stop_) +
+         " kind=" + (direct ? "direct" : "ring") + extra);
     return hipSuccess;
   }
   hipError_t BlocksPerCu(int* per_cu, const void*, int) override {

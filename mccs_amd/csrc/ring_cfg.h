@@ -101,3 +101,60 @@ struct mccsMultiLaunchArgs {
 #ifdef __cplusplus
 static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must stay within 4 KiB");
 #endif
+
+// ---- Direct (two-shot) AllReduce on a fully connected node (direct_kernel.h)
+// Every rank reaches every peer's arena over its own xGMI link, so instead of
+// 2(n-1) ring hops a bucket takes two: each rank writes every chunk it does
+// not own into the owner's "in" slots (all links at once), each owner
+// reduces its chunks in exactly the ring's order (all_reduce.h chunk
+// ownership and summation order, so results are bit-identical to the ring
+// and the oracle) and writes the result into every peer's "out" slot, and
+// every rank copies the results it does not own to its output.  Per-rank
+// link bytes 2(n-1)/n*S, as the ring's.  Used for buckets up to the
+// communicator's direct capacity (MCCS_DIRECT_MAX bytes).
+//
+// A rank's direct region (in its FIFO arena, after the ring's data):
+//   [control, MCCS_DIRECT_CTRL_BYTES]
+//   [in : MCCS_DIRECT_MAX_RANKS senders x slot_bytes]  (by element offset)
+//   [out: slot_bytes]
+// Launch seq s (1, 2, ...) is kept in the control block and advanced by the
+// last workgroup of every launch (graph replays keep counting); flags hold the
+// seq they announce and are waited on with >=.  One set of slots suffices:
+// a rank's in slots are refilled (phase 1 of launch s+1, which waits for
+// nothing) only by a peer that finished launch s, i.e. saw this rank's out
+// flag of s, posted after this rank's last read of its in slots; its out slot
+// is refilled (phase 2 of s+1) only by an owner that saw this rank's in flag
+// of s+1, posted after this rank finished launch s.  Counters are this rank's
+// own and reset by the workgroup that completes them, before the launch ends.
+#define MCCS_DIRECT_MAX_RANKS 8
+#define MCCS_DIRECT_CTRL_BYTES 65536
+#define MCCS_DIRECT_IN_FLAG(s) ((s) * MCCS_FLAG_LINE_BYTES)              // posted by sender s
+#define MCCS_DIRECT_OUT_FLAG(s) (1024 + (s) * MCCS_FLAG_LINE_BYTES)      // posted by owner s
+#define MCCS_DIRECT_CNT_IN(t) (2048 + (t) * MCCS_FLAG_LINE_BYTES)        // our workgroups done writing t's in slot
+#define MCCS_DIRECT_CNT_OUT(t) (3072 + (t) * MCCS_FLAG_LINE_BYTES)       // ... t's out slot
+#define MCCS_DIRECT_DONE 4096
+#define MCCS_DIRECT_LAUNCHES 4224
+#define MCCS_DIRECT_SLOTS (MCCS_DIRECT_MAX_RANKS + 1)
+#define MCCS_DIRECT_THREADS 512
+
+struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
+  const void* send;
+  void* recv;
+  char* region[MCCS_DIRECT_MAX_RANKS];  // every rank's direct region as this rank maps it
+  struct mccsDevComm* comm;             // abortFlag
+  uint32_t rank;
+  uint32_t err_line;
+};
+struct mccsDirectArgs {
+  struct mccsDirectRank r[MCCS_MULTI_MAX_RANKS];
+  uint64_t count;          // elements
+  uint64_t slot_bytes;     // bytes of one in/out slot (>= count * element size)
+  uint64_t timeout_ticks;  // s_memrealtime ticks; 0 = never
+  uint32_t nranks, nch, nthr_ref, buff_size;  // the ring walk this launch reproduces
+  uint32_t fence_mode;                        // MCCS_FENCE_*
+  uint32_t pad;
+  uint8_t idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];  // rank at ring index k of channel bid
+};
+#ifdef __cplusplus
+static_assert(sizeof(mccsDirectArgs) <= 4096, "direct launch arguments must stay within 4 KiB");
+#endif

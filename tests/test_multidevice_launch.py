@@ -290,3 +290,62 @@ def test_fused_ranks_record_their_events_only_when_consumed(fake):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_direct_allreduce_plans(fake):
+    """With a direct threshold, one AllReduce of at most that many bytes per
+    rank launches the direct kernel (one launch per device, the ring walk's
+    channels and thread count in its arguments); a larger one, or two
+    AllReduces of one comm in a group, the ring."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(direct_bytes=4 << 20))
+    try:
+        _log()
+        _allreduce_group(comms, count=1 << 20)  # 4 MiB fp32: direct
+        ev = _log()
+        launches = [kv for k, kv in ev if k == "launch"]
+        assert len(launches) == 8 and all(kv["kind"] == "direct" for kv in launches), launches
+        nch, nthr = C.task_schema(4 << 20, comms[0].nchannels)
+        for kv in launches:
+            assert kv["grid"].endswith("x1") and kv["block"] == "512" and kv["comms_on_dev"] == "1"
+            assert (int(kv["nch"]), int(kv["nthr"]), int(kv["count"])) == (nch, nthr, 1 << 20)
+        assert all(c.last_algo() == "direct" for c in comms)
+        _allreduce_group(comms, count=(1 << 20) + 1)  # one element over: ring
+        ev = _log()
+        assert [kv["kind"] for k, kv in ev if k == "launch"] == ["ring"] * 8
+        assert all(c.last_algo() == "ring" for c in comms)
+        with C.group():  # two AllReduces of each comm: batched for the ring
+            for r, c in enumerate(comms):
+                for j in range(2):
+                    C.all_reduce(c, 0x10000000 * (r + 1) + j * 0x1000000, 0x10000000 * (r + 1) + 0x8000000, 1000, F32,
+                                 SUM, stream=0)
+        ev = _log()
+        assert [kv["kind"] for k, kv in ev if k == "launch"] == ["ring"] * 8
+        for c in comms:
+            c.sync()
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_direct_off_by_default_and_fused_ranks(fake):
+    fake(2)
+    comms = C.init_all([0, 0, 0, 0, 1, 1, 1, 1], C.CommConfig(direct_bytes=1 << 20))
+    plain = None
+    try:
+        _log()
+        _allreduce_group(comms, count=1000)
+        launches = [kv for k, kv in _log() if k == "launch"]
+        assert len(launches) == 2 and all(kv["kind"] == "direct" for kv in launches)
+        assert all(kv["grid"].endswith("x4") and kv["comms_on_dev"] == "1" for kv in launches)
+        for c in comms:
+            c.sync()
+        plain = C.init_all([0, 1])  # library default: no direct region, ring only
+        _log()
+        _allreduce_group(plain, count=1000)
+        assert [kv["kind"] for k, kv in _log() if k == "launch"] == ["ring"] * 2
+        for c in plain:
+            c.sync()
+    finally:
+        for c in comms + (plain or []):
+            c.destroy()
