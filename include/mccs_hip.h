@@ -112,8 +112,8 @@ typedef struct mccsComm *mccsComm_t;
 
 /* Communicator profile: comm_default_config (mccs.toml:18-20, config.rs:15-97)
  * plus the MI355X execution knobs.  Zero fields take defaults.
- * ABI note: `fifo_slots` and `direct_bytes` were appended in library version
- * 0.3, which grew the struct; mccsCommConfigDefault() writes sizeof(mccsCommConfig) bytes, so a
+ * ABI note: `fifo_slots`, `direct_bytes` and `oneshot_bytes` were appended in
+ * library version 0.3, which grew the struct; mccsCommConfigDefault() writes sizeof(mccsCommConfig) bytes, so a
  * caller compiled against an older header must be rebuilt.  Callers binding
  * the struct by hand (ctypes, bindgen) check mccsCommConfigSize(). */
 typedef struct {
@@ -137,6 +137,10 @@ typedef struct {
                            output equals the ring's bit for bit; larger buckets take the ring.
                            0 = default (MCCS_DIRECT_BYTES), < 0 = never.  Every rank must agree
                            (it sizes the arena: Connect refuses a mismatch) */
+  int oneshot_bytes;    /* buckets of at most this many bytes per rank take the one-shot variant
+                           instead: every rank sends its whole input to every peer and reduces
+                           every chunk itself (same order, same bits; one exchange instead of
+                           two).  0 = default (MCCS_ONESHOT_BYTES), < 0 = never; ranks must agree */
 } mccsCommConfig;
 
 void mccsCommConfigDefault(mccsCommConfig *cfg);
@@ -182,10 +186,11 @@ mccsResult_t mccsCommDestroy(mccsComm_t comm);
 mccsResult_t mccsCommInfo(mccsComm_t comm, int *info7);
 /* ring send order of channel ch (nranks ints). */
 mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int *order);
-/* Algorithm of the comm's latest launch: MCCS_ALGO_RING or MCCS_ALGO_DIRECT
- * (-1 before the first). */
+/* Algorithm of the comm's latest launch: MCCS_ALGO_RING, MCCS_ALGO_DIRECT
+ * (two-shot) or MCCS_ALGO_ONESHOT (-1 before the first). */
 #define MCCS_ALGO_RING 0
 #define MCCS_ALGO_DIRECT 1
+#define MCCS_ALGO_ONESHOT 2
 int mccsCommLastAlgo(mccsComm_t comm);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);

@@ -70,7 +70,8 @@ class _CommConfig(ctypes.Structure):
     _fields_ = [("channel_count", _c_int), ("buffer_size", _c_int), ("lanes", _c_int),
                 ("block_threads", _c_int), ("locality", _c_int), ("fifo_memory", _c_int),
                 ("timeout_ms", _c_int), ("work_fifo_depth", _c_int), ("bridge_streams", _c_int),
-                ("rings", _P(_c_int)), ("fifo_slots", _c_int), ("direct_bytes", _c_int)]
+                ("rings", _P(_c_int)), ("fifo_slots", _c_int), ("direct_bytes", _c_int),
+                ("oneshot_bytes", _c_int)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/mccs_hip.h

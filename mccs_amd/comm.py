@@ -82,6 +82,7 @@ class CommConfig:
     rings: list | None = None  # comm_patterns_override: channel_count x nranks send orders
     fifo_slots: int | None = None  # FIFO slots per connection: 8 (reference), 16, 32
     direct_bytes: int | None = None  # largest bucket (bytes per rank) for the direct two-shot kernel; < 0 never
+    oneshot_bytes: int | None = None  # largest bucket for the one-shot variant; < 0 never
 
     def to_c(self, nranks: int):
         c = _CommConfig()
@@ -145,9 +146,10 @@ class Communicator:
         return out
 
     def last_algo(self) -> str | None:
-        """"ring" or "direct": the algorithm of the latest launch (None before one)."""
+        """"ring", "direct" (two-shot) or "oneshot": the algorithm of the latest
+        launch (None before one)."""
         a = _sig().mccsCommLastAlgo(self._h)
-        return {0: "ring", 1: "direct"}.get(a)
+        return {0: "ring", 1: "direct", 2: "oneshot"}.get(a)
 
     def dev_comm(self) -> int:
         p = ctypes.c_void_p()

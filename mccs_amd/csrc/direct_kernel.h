@@ -1,45 +1,55 @@
-// direct_kernel.h — two-shot ("direct") AllReduce for a fully connected node.
+// direct_kernel.h — direct AllReduce (two-shot / one-shot) for a fully
+// connected node.
 //
 // The ring (ring_kernel.h, all_reduce.h) moves a bucket through 2(n-1)
 // neighbour hops.  On an MI355X node every GPU has a link to every other, so
-// here a bucket takes two (ring_cfg.h, "Direct"): scatter every chunk to its
-// owner, reduce, and broadcast the result.  What it keeps from the reference
-// is everything that decides a result bit for bit: the ring's chunk walk
-// (all_reduce.h:28-42: chunkSize, loopSize, realChunkSize rounding, chunk k of
-// channel bid at gridOffset + (bid*n + k)*realChunkSize), chunk k's owner (the
-// rank at ring index k of channel bid's ring) and its summation order
-// (acc = x[idx k+1]; acc = fn(x[idx k+j], acc) for j = 2..n, rounded in T at
-// every step, all_reduce.h:46-70 + prims_simple.h:174-177), so the output
-// equals the ring's (and the oracle's) for the same channels and rings.
+// here a bucket takes two (two-shot) or one (one-shot) -- ring_cfg.h,
+// "Direct AllReduce", has the region layout and the reuse argument.  What it
+// keeps from the reference is everything that decides a result bit for bit:
+// the ring's chunk walk (all_reduce.h:28-42: chunkSize, loopSize,
+// realChunkSize rounding, chunk k of channel bid at gridOffset +
+// (bid*n + k)*realChunkSize), chunk k's owner (the rank at ring index k of
+// channel bid's ring) and its summation order (acc = x[idx k+1];
+// acc = fn(x[idx k+j], acc) for j = 2..n, rounded in T at every step,
+// all_reduce.h:46-70 + prims_simple.h:174-177), so the output equals the
+// ring's (and the oracle's) for the same channels and rings.
 //
 // One launch per device (blockIdx.y = rank slot when ranks share a GPU), G
-// workgroups per rank of MCCS_DIRECT_THREADS threads; sub-tiles of every
-// chunk are dealt to the workgroups round-robin.  Phases, per workgroup:
-//   1. copy its sub-tiles of chunks owned by others into the owner's in slot
-//      (remote stores over xGMI); drain; count itself out per owner -- the
-//      workgroup that completes an owner's count posts that owner's in flag;
-//   2. for its sub-tiles of chunks it owns: wait for every in flag, reduce the
-//      n sources in the ring's order (own input read locally, the others from
-//      its own in slots), store to the output and to every peer's out slot;
-//      drain; count out per peer -- the last posts the peer's out flag;
-//   3. for its sub-tiles of chunks owned by others: wait for that owner's out
-//      flag, copy the result from its out slot to the output.
-// Flags hold the launch sequence number (>= seq = ready; ring_cfg.h has why
-// one set of slots is safe across back-to-back launches).  The hand-off
-// policy follows the ring's (mccsRingKernelCfg fence modes): drains only for
-// uncached arenas, a system-scope release before counting out and an acquire
-// after a wait otherwise (each workgroup fences its own writes: a release only
-// writes back the issuing XCD's L2).
+// workgroups per rank of MCCS_DIRECT_THREADS threads.  Each phase cuts the
+// chunks it touches into pieces and deals them to the G workgroups
+// round-robin, so every phase is spread over all of them.
+//   two-shot
+//     1. scatter: pieces of chunks owned by others -> the owner's in slot
+//        (remote stores over xGMI); drain; add the elements written to each
+//        owner's IN_CNT line;
+//     2. reduce: wait until every peer has sent this rank its chunks; for
+//        pieces of the chunks this rank owns, reduce the n sources in the
+//        ring's order (own input local, the others from its in slots), store
+//        to the output and every peer's out slot; drain; add to every peer's
+//        OUT_CNT line;
+//     3. gather: wait for every owner's broadcast; copy the results of
+//        chunks owned by others from the out slot to the output.
+//     Phases 1 and 3 deal the same chunks with the same pieces, so a
+//     workgroup rewrites in phase 3 exactly what it read in phase 1 (an
+//     in-place call is safe).
+//   one-shot (small buckets)
+//     1. broadcast: pieces of the whole input -> every peer's one-shot slot
+//        of this launch's parity; drain; add to every peer's IN_CNT line;
+//     2. reduce: wait for every peer's input; every chunk, in the ring's
+//        order, straight into the output.
+// The hand-off policy follows the ring's (mccsRingKernelCfg fence modes):
+// drains only for uncached arenas, a system-scope release before the count
+// and an acquire after a wait otherwise (each workgroup fences its own
+// writes: a release only writes back the issuing XCD's L2).
 #pragma once
 #include "ring_kernel.h"
 
 namespace mccs {
 
-constexpr int64_t kDirectSubBytes = 64 * 1024;  // sub-tile of a chunk dealt to one workgroup
-constexpr int kDirectUnroll = 2;                 // packs per lane per source in flight (x up to 8 sources)
+constexpr int kDirectUnroll = 2;  // packs per lane per source in flight (x up to 8 sources)
 
 struct DirectWalk {
-  int64_t size, chunkSize, loopSize, gran, sub;
+  int64_t size, chunkSize, loopSize, gran;
   int n, nch;
 };
 
@@ -56,16 +66,12 @@ __device__ __forceinline__ DirectWalk direct_walk(const mccsDirectArgs& a) {
   w.loopSize = (int64_t)w.nch * w.n * w.chunkSize;
   w.gran = (int64_t)((int)a.nthr_ref - WARP_SIZE) * 8 / (int64_t)sizeof(T);
   if (w.gran < 1) w.gran = 1;
-  w.sub = kDirectSubBytes / (int64_t)sizeof(T);
   return w;
 }
 
-// Calls f(item, off, nelem, bid, k) for every sub-tile of every chunk in the
-// ring's walk order; `item` numbers them 0, 1, ... identically in every
-// workgroup and on every rank.
+// Calls f(off, nelem, bid, k, owner) for every chunk of the ring's walk, in order.
 template <typename F>
-__device__ __forceinline__ void direct_items(const DirectWalk& w, F&& f) {
-  uint32_t item = 0;
+__device__ __forceinline__ void direct_chunks(const DirectWalk& w, const mccsDirectArgs& a, F&& f) {
   for (int64_t g = 0; g < w.size; g += w.loopSize) {
     int64_t rcs = div_up(w.size - g, (int64_t)w.nch * w.n);  // realChunkSize, all_reduce.h:30-36
     rcs = w.chunkSize < rcs ? w.chunkSize : rcs;
@@ -74,41 +80,75 @@ __device__ __forceinline__ void direct_items(const DirectWalk& w, F&& f) {
       for (int k = 0; k < w.n; ++k) {
         const int64_t off = g + ((int64_t)bid * w.n + k) * rcs;
         const int64_t ne = rcs < w.size - off ? rcs : w.size - off;
-        for (int64_t s = 0; s < ne; s += w.sub) f(item++, off + s, ne - s < w.sub ? ne - s : w.sub, bid, k);
+        if (ne > 0) f(off, ne, bid, k, (uint32_t)a.idx2rank[bid][k]);
       }
   }
 }
 
+// This workgroup's pieces (pc elements) of the chunks `want(owner)` selects:
+// the selected chunks' pieces are numbered 0, 1, ... in walk order and piece
+// p goes to workgroup p % G.  Calls f(off, nelem, bid, k, owner).
+template <typename W, typename F>
+__device__ __forceinline__ void direct_pieces(const DirectWalk& w, const mccsDirectArgs& a, int64_t pc, uint32_t G,
+                                              uint32_t bx, W&& want, F&& f) {
+  uint64_t base = 0;  // pieces of selected chunks before this one
+  direct_chunks(w, a, [&](int64_t off, int64_t ne, int bid, int k, uint32_t owner) {
+    if (!want(owner)) return;
+    const int64_t np = div_up(ne, pc);
+    for (int64_t j = (int64_t)((bx + G - (uint32_t)(base % G)) % G); j < np; j += G) {
+      const int64_t s = j * pc;
+      f(off + s, ne - s < pc ? ne - s : pc, bid, k, owner);
+    }
+    base += (uint64_t)np;
+  });
+}
+
 struct DirectShm {
   uint64_t seq;
+  uint64_t e_in;                            // E_IN at launch start
+  uint64_t e_out[MCCS_DIRECT_MAX_RANKS];    // E_OUT at launch start
+  uint64_t owned[MCCS_DIRECT_MAX_RANKS];    // elements of this launch's chunks each rank owns
+  uint64_t sent[MCCS_DIRECT_MAX_RANKS];     // elements this workgroup wrote into each rank's slots (this phase)
   int ok;  // 0 after an abort / watchdog (written by thread 0 inside direct_wait only)
 };
 
-// Thread 0 spins until *flag >= seq; the whole workgroup then agrees.
-__device__ __forceinline__ bool direct_wait(DirectShm& sh, const uint64_t* flag, uint64_t seq,
-                                            volatile uint32_t* abortFlag, const mccsDirectArgs& a,
-                                            const mccsRingKernelCfg& ecfg) {
-  if (threadIdx.x == 0 && sh.ok) {
+// Wave 0 spins until, for every rank t in `mask`, the u64 count at
+// ctrl + cnt_base + t x line reaches need[t]; lane t polls rank t, so all
+// counts cost one round trip per poll.  The whole workgroup then agrees.
+__device__ __forceinline__ bool direct_wait(DirectShm& sh, const char* ctrl, int cnt_base, uint32_t mask,
+                                            const uint64_t* need_sh, volatile uint32_t* abortFlag,
+                                            const mccsDirectArgs& a, const mccsRingKernelCfg& ecfg) {
+  if (threadIdx.x < 64 && sh.ok) {
+    const uint32_t lane = threadIdx.x;
+    const bool poll = lane < MCCS_DIRECT_MAX_RANKS && ((mask >> lane) & 1u);
+    const uint64_t need = poll ? need_sh[lane] : 0;
+    const uint64_t* cnt = (const uint64_t*)(ctrl + cnt_base + (poll ? lane : 0) * MCCS_FLAG_LINE_BYTES);
     const bool uncached = a.fence_mode != MCCS_FENCE_SYSTEM;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t attempt = 0, spins = 0;
-    while (ld_poll(flag, uncached, attempt++) < seq) {
+    int failed = 0;
+    while (!__all(!poll || ld_poll(cnt, uncached, attempt) >= need)) {
+      ++attempt;
       if (++spins >= 64) {
         spins = 0;
-        if (abort_raised(abortFlag)) {
-          raise_error(abortFlag, ecfg, MCCS_ERR_ABORTED);
-          sh.ok = 0;
-          break;
+        int why = 0;  // decided by lane 0, taken by every lane
+        if (lane == 0) {
+          if (abort_raised(abortFlag)) why = 1;
+          else if (a.timeout_ticks && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) why = 2;
+          if (why) raise_error(abortFlag, ecfg, why == 1 ? MCCS_ERR_ABORTED : MCCS_ERR_TIMEOUT);
         }
-        if (a.timeout_ticks && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-          raise_error(abortFlag, ecfg, MCCS_ERR_TIMEOUT);
-          sh.ok = 0;
+        why = __builtin_amdgcn_readfirstlane(why);
+        if (why) {
+          failed = 1;
           break;
         }
       }
       __builtin_amdgcn_s_sleep(MCCS_POLL_SLEEP);
     }
-    if (sh.ok && !uncached) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (lane == 0) {
+      if (failed) sh.ok = 0;
+      else if (!uncached) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
   }
   __syncthreads();
   const bool ok = sh.ok != 0;
@@ -117,32 +157,31 @@ __device__ __forceinline__ bool direct_wait(DirectShm& sh, const uint64_t* flag,
 }
 
 // This workgroup's writes of the phase are complete (and, for cached arenas,
-// written back); count it out for every target rank.  The workgroup that
-// completes a target's count resets it (for the next launch) and posts
-// `seq` into the target's flag line.
+// written back): add what it wrote into each rank's slots (sh.sent) to that
+// rank's count line for this rank (lane t of wave 0 for rank t: one remote
+// atomic each, no return value awaited), then clear sh.sent.
 __device__ __forceinline__ void direct_count_out(DirectShm& sh, const mccsDirectArgs& a, const mccsDirectRank& me,
-                                                 char* ctrl, int cnt_base, int flag_base, uint64_t seq) {
+                                                 int cnt_base) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0 && sh.ok) {
+  if (threadIdx.x < 64 && sh.ok) {
     if (a.fence_mode != MCCS_FENCE_UNCACHED) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    for (uint32_t t = 0; t < a.nranks; ++t) {
-      if (t == me.rank) continue;
-      uint32_t* cnt = (uint32_t*)(ctrl + cnt_base + (int)t * MCCS_FLAG_LINE_BYTES);
-      const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old + 1 == gridDim.x) {
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        st_flag((uint64_t*)(me.region[t] + flag_base + (int)me.rank * MCCS_FLAG_LINE_BYTES), seq);
-      }
-    }
+    const uint32_t t = threadIdx.x;
+    if (t < a.nranks && t != me.rank && sh.sent[t])
+      __hip_atomic_fetch_add((uint64_t*)(me.region[t] + cnt_base + (int)me.rank * MCCS_FLAG_LINE_BYTES), sh.sent[t],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  __syncthreads();
+  if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) sh.sent[threadIdx.x] = 0;
+  __syncthreads();
 }
 
-// Phase 2 of one sub-tile: acc = x[q1]; acc = fn(x[qj], acc) (j = 2..n) over
-// the sources in ring order, stored to the output and every peer's out slot.
+// acc = x[src0]; acc = fn(x[srcj], acc) (j = 1..n-1) over the sources in
+// ring order, stored to every non-null destination among dst[0 .. ndst)
+// (n = 1: a copy to several places).
 template <int DT, int OP>
 __device__ __forceinline__ void direct_reduce(const void* const* src, int n, void* const* dst, int ndst, int64_t ne) {
   using T = typename Elem<DT>::T;
@@ -177,7 +216,7 @@ __device__ __forceinline__ void direct_reduce(const void* const* src, int n, voi
           if (j < n) acc = pack_op<DT, OP>(v[j][u], acc);
 #pragma unroll
         for (int d = 0; d < MCCS_DIRECT_MAX_RANKS; ++d)
-          if (d < ndst) ((u32x4*)dst[d])[base + (int64_t)u * nthr] = acc;
+          if (d < ndst && dst[d]) ((u32x4*)dst[d])[base + (int64_t)u * nthr] = acc;
       }
     }
     done = npack * PACK;
@@ -189,7 +228,7 @@ __device__ __forceinline__ void direct_reduce(const void* const* src, int n, voi
       if (j < n) acc = scalar_op<DT, OP>(__builtin_nontemporal_load((const T*)src[j] + e), acc);
 #pragma unroll
     for (int d = 0; d < MCCS_DIRECT_MAX_RANKS; ++d)
-      if (d < ndst) ((T*)dst[d])[e] = acc;
+      if (d < ndst && dst[d]) ((T*)dst[d])[e] = acc;
   }
 }
 
@@ -203,91 +242,157 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   volatile uint32_t* abortFlag = me.comm ? me.comm->abortFlag : nullptr;
   mccsRingKernelCfg ecfg{};
   ecfg.err_line = me.err_line;
+  const DirectWalk w = direct_walk<DT>(a);
+  const bool one_shot = a.mode == MCCS_DIRECT_ONE_SHOT;
   if (threadIdx.x == 0) {
-    sh.seq = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_LAUNCHES), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT) + 1;
+    sh.seq = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_LAUNCHES), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    sh.e_in = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_E_IN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh.ok = !abort_raised(abortFlag);
+    for (int t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t) {
+      sh.e_out[t] = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_E_OUT(t)), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+      sh.owned[t] = 0;
+      sh.sent[t] = 0;
+    }
+    direct_chunks(w, a, [&](int64_t, int64_t ne, int, int, uint32_t owner) { sh.owned[owner] += (uint64_t)ne; });
   }
   __syncthreads();
   const uint64_t seq = sh.seq;
   const int64_t esz = (int64_t)sizeof(T);
-  const int64_t slot = (int64_t)a.slot_bytes;
-  auto in_slot = [&](char* region, uint32_t sender) {
-    return region + MCCS_DIRECT_CTRL_BYTES + (int64_t)sender * slot;
-  };
-  auto out_slot = [&](char* region) {
-    return region + MCCS_DIRECT_CTRL_BYTES + (int64_t)MCCS_DIRECT_MAX_RANKS * slot;
-  };
-  const DirectWalk w = direct_walk<DT>(a);
   const uint32_t G = gridDim.x, bx = blockIdx.x;
+  const uint32_t peers = ((1u << n) - 1u) & ~(1u << me.rank);
+  const int64_t piece = a.piece > 0 ? (int64_t)a.piece : 1;
+  const int64_t piece2 = a.piece2 > 0 ? (int64_t)a.piece2 : 1;
   u32x4 nopre[1];
+  __shared__ uint64_t need[MCCS_DIRECT_MAX_RANKS];
 
-  // 1. scatter: every chunk owned by another rank goes to its owner's in slot
-  direct_items(w, [&](uint32_t item, int64_t off, int64_t ne, int bid, int k) {
-    if (item % G != bx || !sh.ok) return;
-    const uint32_t owner = a.idx2rank[bid][k];
-    if (owner == me.rank) return;
-    reduce_copy_rows<DT, OpSum, MCCS_RING_UNROLL, 1, 1, MCCS_RING_INPUT_NT, kPlain>(
-        (const T*)me.send + off, nullptr, in_slot(me.region[owner], me.rank) + off * esz, nullptr, ne, threadIdx.x,
-        blockDim.x, false, nopre);
-  });
-  direct_count_out(sh, a, me, mine, MCCS_DIRECT_CNT_IN(0), MCCS_DIRECT_IN_FLAG(0), seq);
-
-  // 2. reduce the chunks this rank owns, in the ring's order
-  bool in_seen = false;  // uniform across the workgroup, like `seen` below
-  direct_items(w, [&](uint32_t item, int64_t off, int64_t ne, int bid, int k) {
-    if (item % G != bx || !sh.ok) return;
-    if (a.idx2rank[bid][k] != me.rank) return;
-    if (!in_seen) {
-      for (int s = 0; s < n; ++s)
-        if (s != (int)me.rank &&
-            !direct_wait(sh, (const uint64_t*)(mine + MCCS_DIRECT_IN_FLAG(s)), seq, abortFlag, a, ecfg))
-          return;
-      in_seen = true;
-    }
-    // sources in the ring's order from ring index k+1; destinations: the
-    // output, then every peer's out slot
-    const void* src[MCCS_DIRECT_MAX_RANKS];
-    void* dst[MCCS_DIRECT_MAX_RANKS];
+  if (one_shot) {
+    const int64_t oslot = (int64_t)a.oslot_bytes;
+    const int64_t obase = MCCS_DIRECT_CTRL_BYTES + (int64_t)MCCS_DIRECT_SLOTS * (int64_t)a.slot_bytes +
+                          (int64_t)(seq & 1) * MCCS_DIRECT_MAX_RANKS * oslot;
+    // 1. broadcast the whole input: pieces of [0, count) to every peer's slot
+    const int64_t np = div_up(w.size, piece);
+    for (int64_t j = bx; j < np && sh.ok; j += G) {
+      const int64_t off = j * piece, ne = w.size - off < piece ? w.size - off : piece;
+      const void* src[MCCS_DIRECT_MAX_RANKS] = {(const T*)me.send + off};
+      void* dst[MCCS_DIRECT_MAX_RANKS];  // slot t: rank t's one-shot slot (none for this rank)
 #pragma unroll
-    for (int j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j) {
-      src[j] = nullptr;
-      dst[j] = nullptr;
-      if (j < n) {
-        int idx = k + 1 + j;
-        idx = idx >= n ? idx - n : idx;
-        const uint32_t q = a.idx2rank[bid][idx];
-        src[j] = q == me.rank ? (const void*)((const T*)me.send + off) : (const void*)(in_slot(mine, q) + off * esz);
-        // slot j of dst: rank j (own -> the output)
-        dst[j] = j == (int)me.rank ? (void*)((T*)me.recv + off) : (void*)(out_slot(me.region[j]) + off * esz);
+      for (int t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
+        dst[t] = t < n && t != (int)me.rank ? me.region[t] + obase + (int64_t)me.rank * oslot + off * esz : nullptr;
+      direct_reduce<DT, OpSum>(src, 1, dst, n, ne);
+      if (threadIdx.x == 0)
+        for (int t = 0; t < n; ++t) sh.sent[t] += (uint64_t)ne;
+    }
+    direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
+    // 2. every chunk, reduced in the ring's order into the output
+    if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + (uint64_t)w.size;
+    __syncthreads();
+    bool in_seen = false;  // uniform across the workgroup
+    direct_pieces(w, a, piece2, G, bx, [](uint32_t) { return true; },
+                  [&](int64_t off, int64_t ne, int bid, int k, uint32_t) {
+                    if (!sh.ok) return;
+                    if (!in_seen) {
+                      if (!direct_wait(sh, mine, MCCS_DIRECT_IN_CNT(0), peers, need, abortFlag, a, ecfg)) return;
+                      in_seen = true;
+                    }
+                    const void* src[MCCS_DIRECT_MAX_RANKS];
+                    void* dst[MCCS_DIRECT_MAX_RANKS] = {(T*)me.recv + off};
+#pragma unroll
+                    for (int j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j) {
+                      src[j] = nullptr;
+                      if (j < n) {
+                        int idx = k + 1 + j;
+                        idx = idx >= n ? idx - n : idx;
+                        const uint32_t q = a.idx2rank[bid][idx];
+                        src[j] = q == me.rank ? (const void*)((const T*)me.send + off)
+                                              : (const void*)(mine + obase + (int64_t)q * oslot + off * esz);
+                      }
+                    }
+                    direct_reduce<DT, OP>(src, n, dst, 1, ne);
+                  });
+  } else {
+    const int64_t slot = (int64_t)a.slot_bytes;
+    auto in_slot = [&](char* region, uint32_t sender) {
+      return region + MCCS_DIRECT_CTRL_BYTES + (int64_t)sender * slot;
+    };
+    auto out_slot = [&](char* region) {
+      return region + MCCS_DIRECT_CTRL_BYTES + (int64_t)MCCS_DIRECT_MAX_RANKS * slot;
+    };
+    auto others = [&](uint32_t owner) { return owner != me.rank; };
+    auto own = [&](uint32_t owner) { return owner == me.rank; };
+
+    // 1. scatter: every chunk owned by another rank goes to its owner's in slot
+    direct_pieces(w, a, piece, G, bx, others, [&](int64_t off, int64_t ne, int, int, uint32_t owner) {
+      if (!sh.ok) return;
+      reduce_copy_rows<DT, OpSum, MCCS_RING_UNROLL, 1, 1, MCCS_RING_INPUT_NT, kPlain>(
+          (const T*)me.send + off, nullptr, in_slot(me.region[owner], me.rank) + off * esz, nullptr, ne, threadIdx.x,
+          blockDim.x, false, nopre);
+      if (threadIdx.x == 0) sh.sent[owner] += (uint64_t)ne;
+    });
+    direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
+
+    // 2. reduce the chunks this rank owns, in the ring's order; broadcast
+    if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + sh.owned[me.rank];
+    __syncthreads();
+    bool in_seen = false;  // uniform across the workgroup, like out_seen below
+    direct_pieces(w, a, piece2, G, bx, own, [&](int64_t off, int64_t ne, int bid, int k, uint32_t) {
+      if (!sh.ok) return;
+      if (!in_seen) {
+        if (!direct_wait(sh, mine, MCCS_DIRECT_IN_CNT(0), peers, need, abortFlag, a, ecfg)) return;
+        in_seen = true;
       }
-    }
-    direct_reduce<DT, OP>(src, n, dst, n, ne);
-  });
-  direct_count_out(sh, a, me, mine, MCCS_DIRECT_CNT_OUT(0), MCCS_DIRECT_OUT_FLAG(0), seq);
+      // sources in the ring's order from ring index k+1; destination slot t:
+      // rank t's out slot (own: the output)
+      const void* src[MCCS_DIRECT_MAX_RANKS];
+      void* dst[MCCS_DIRECT_MAX_RANKS];
+#pragma unroll
+      for (int j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j) {
+        src[j] = nullptr;
+        dst[j] = nullptr;
+        if (j < n) {
+          int idx = k + 1 + j;
+          idx = idx >= n ? idx - n : idx;
+          const uint32_t q = a.idx2rank[bid][idx];
+          src[j] = q == me.rank ? (const void*)((const T*)me.send + off) : (const void*)(in_slot(mine, q) + off * esz);
+          dst[j] = j == (int)me.rank ? (void*)((T*)me.recv + off) : (void*)(out_slot(me.region[j]) + off * esz);
+        }
+      }
+      direct_reduce<DT, OP>(src, n, dst, n, ne);
+      if (threadIdx.x == 0)
+        for (int t = 0; t < n; ++t) sh.sent[t] += (uint64_t)ne;
+    });
+    direct_count_out(sh, a, me, MCCS_DIRECT_OUT_CNT(0));
 
-  // 3. gather: results of the chunks owned by others, from this rank's out slot
-  uint32_t seen = 0;  // owners whose out flag this workgroup has seen
-  direct_items(w, [&](uint32_t item, int64_t off, int64_t ne, int bid, int k) {
-    if (item % G != bx || !sh.ok) return;
-    const uint32_t owner = a.idx2rank[bid][k];
-    if (owner == me.rank) return;
-    if (!(seen & (1u << owner))) {
-      if (!direct_wait(sh, (const uint64_t*)(mine + MCCS_DIRECT_OUT_FLAG(owner)), seq, abortFlag, a, ecfg))
-        return;
-      seen |= 1u << owner;
-    }
-    reduce_copy_rows<DT, OpSum, MCCS_RING_UNROLL, 1, 1, 1, MCCS_RING_OUT_POLICY>(
-        out_slot(mine) + off * esz, nullptr, (T*)me.recv + off, nullptr, ne, threadIdx.x, blockDim.x, false, nopre);
-  });
+    // 3. gather: results of the chunks owned by others, from this rank's out slot
+    if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_out[threadIdx.x] + sh.owned[threadIdx.x];
+    __syncthreads();
+    bool out_seen = false;
+    direct_pieces(w, a, piece, G, bx, others, [&](int64_t off, int64_t ne, int, int, uint32_t) {
+      if (!sh.ok) return;
+      if (!out_seen) {
+        if (!direct_wait(sh, mine, MCCS_DIRECT_OUT_CNT(0), peers, need, abortFlag, a, ecfg)) return;
+        out_seen = true;
+      }
+      reduce_copy_rows<DT, OpSum, MCCS_RING_UNROLL, 1, 1, 1, MCCS_RING_OUT_POLICY>(
+          out_slot(mine) + off * esz, nullptr, (T*)me.recv + off, nullptr, ne, threadIdx.x, blockDim.x, false, nopre);
+    });
+  }
 
-  // the launch is over for this workgroup: the last one advances the sequence
+  // the launch is over for this workgroup: the last one advances the running
+  // totals and the launch count (read by the next launch, after this one)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0 && sh.ok) {
     uint32_t* done = (uint32_t*)(mine + MCCS_DIRECT_DONE);
     if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == G) {
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_IN),
+                         sh.e_in + (one_shot ? (uint64_t)w.size : sh.owned[me.rank]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (!one_shot)
+        for (int t = 0; t < n; ++t)
+          __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_OUT(t)), sh.e_out[t] + sh.owned[t], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_LAUNCHES), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -35,6 +35,7 @@ static void group_discard() {
 // Direct AllReduce threshold when the config leaves it 0 (MCCS_DIRECT_BYTES
 // overrides): buckets up to this many bytes per rank take the two-shot kernel.
 static constexpr int kDirectDefaultBytes = 0;
+static constexpr int kOneshotDefaultBytes = 0;  // MCCS_ONESHOT_BYTES
 
 static void fill_defaults(mccsCommConfig* c) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
@@ -50,6 +51,7 @@ static void fill_defaults(mccsCommConfig* c) {
   // (8 MiB per connection)
   if (c->fifo_slots == 0) c->fifo_slots = 2 * MCCS_BUFFER_SLOTS;
   if (c->direct_bytes == 0) c->direct_bytes = kDirectDefaultBytes;
+  if (c->oneshot_bytes == 0) c->oneshot_bytes = kOneshotDefaultBytes;
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
@@ -69,7 +71,8 @@ static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
     return mccsInvalidArgument;
   if (nranks < 1 || nranks > 64) return mccsInvalidArgument;
   if (c.fifo_slots != 8 && c.fifo_slots != 16 && c.fifo_slots != 32) return mccsInvalidArgument;
-  if (c.direct_bytes > (1 << 30)) return mccsInvalidArgument;  // 9 slots of it live in every rank's arena
+  if (c.direct_bytes > (1 << 30)) return mccsInvalidArgument;    // 9 slots of it live in every rank's arena
+  if (c.oneshot_bytes > (64 << 20)) return mccsInvalidArgument;  // 16 slots of it
   return mccsSuccess;
 }
 
@@ -188,7 +191,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   // operator overrides (no rebuild needed): MCCS_LOCALITY=sender|receiver,
   // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE,
   // MCCS_BRIDGE_STREAMS, MCCS_FIFO_MEMORY=uncached|release|device,
-  // MCCS_FIFO_SLOTS, MCCS_DIRECT_BYTES
+  // MCCS_FIFO_SLOTS, MCCS_DIRECT_BYTES, MCCS_ONESHOT_BYTES
   if (const char* v = std::getenv("MCCS_LOCALITY"))
     cfg->locality = (v[0] == 's' || v[0] == 'S') ? MCCS_LOCALITY_SENDER : MCCS_LOCALITY_RECEIVER;
   if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
@@ -202,6 +205,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   if (const char* v = std::getenv("MCCS_BUFFER_SIZE")) cfg->buffer_size = std::atoi(v);
   if (const char* v = std::getenv("MCCS_FIFO_SLOTS")) cfg->fifo_slots = std::atoi(v);
   if (const char* v = std::getenv("MCCS_DIRECT_BYTES")) cfg->direct_bytes = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_ONESHOT_BYTES")) cfg->oneshot_bytes = std::atoi(v);
 }
 
 extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {

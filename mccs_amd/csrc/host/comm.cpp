@@ -195,9 +195,11 @@ mccsResult_t comm_alloc_local(Comm* c) {
   c->layout.buffer_size = (size_t)c->cfg.buffer_size;
   c->layout.fifo_bytes = (size_t)c->cfg.buffer_size / MCCS_BUFFER_SLOTS * (size_t)c->cfg.fifo_slots;
   // direct AllReduce region: only where the kernel can run (2..8 ranks)
-  c->layout.direct_slot = (c->cfg.direct_bytes > 0 && c->nranks >= 2 && c->nranks <= MCCS_DIRECT_MAX_RANKS)
-                              ? ((size_t)c->cfg.direct_bytes + 65535) & ~(size_t)65535
-                              : 0;
+  const bool direct_ok = c->nranks >= 2 && c->nranks <= MCCS_DIRECT_MAX_RANKS;
+  c->layout.direct_slot =
+      direct_ok && c->cfg.direct_bytes > 0 ? ((size_t)c->cfg.direct_bytes + 65535) & ~(size_t)65535 : 0;
+  c->layout.oneshot_slot =
+      direct_ok && c->cfg.oneshot_bytes > 0 ? ((size_t)c->cfg.oneshot_bytes + 65535) & ~(size_t)65535 : 0;
   const size_t bytes = c->layout.total();
   c->own_arena = nullptr;
   c->own_arena_uncached = false;

@@ -117,8 +117,10 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   // One AllReduce that fits the direct region (every rank decides alike: same
   // call, same config) is held for the direct kernel; the launch may still
   // send it to the ring (plan_launch_group).
-  if (!c->plan_pending && func == mccsFuncAllReduce && c->layout.direct_slot > 0 &&
-      count * (size_t)elem_bytes(dtype) <= (size_t)c->cfg.direct_bytes) {
+  const size_t bytes = count * (size_t)elem_bytes(dtype);
+  const bool oneshot = c->layout.oneshot_slot > 0 && bytes <= (size_t)c->cfg.oneshot_bytes;
+  const bool twoshot = c->layout.direct_slot > 0 && bytes <= (size_t)c->cfg.direct_bytes;
+  if (!c->plan_pending && func == mccsFuncAllReduce && (oneshot || twoshot)) {
     c->plan_direct = true;
     c->direct.send = send;
     c->direct.recv = recv;
@@ -393,36 +395,12 @@ static int coresident_direct_blocks(int device) {
   return cache[device] = best * ncu;
 }
 
-// Sub-tiles the direct kernel deals to its workgroups (direct_kernel.h
-// direct_items, the ring's chunk walk cut into 64 KiB pieces).
-static uint32_t direct_item_count(size_t count, size_t esize, int n, int nch, int nthr, int buff) {
-  const int64_t size = (int64_t)count;
-  const int64_t chunk = (int64_t)(buff / MCCS_BUFFER_SLOTS / (int)esize) * ALLREDUCE_CHUNKSTEPS;
-  const int64_t loop = (int64_t)nch * n * chunk;
-  int64_t gran = (int64_t)(nthr - WARP_SIZE) * 8 / (int64_t)esize;
-  if (gran < 1) gran = 1;
-  const int64_t sub = 65536 / (int64_t)esize;
-  uint64_t items = 0;
-  for (int64_t g = 0; g < size; g += loop) {
-    int64_t rcs = (size - g + (int64_t)nch * n - 1) / ((int64_t)nch * n);
-    rcs = std::min(chunk, rcs);
-    rcs = (rcs + gran - 1) / gran * gran;
-    for (int64_t c = 0; c < (int64_t)nch * n; ++c) {
-      const int64_t ne = std::min(rcs, size - (g + c * rcs));
-      if (ne > 0) items += (uint64_t)((ne + sub - 1) / sub);
-    }
-  }
-  return (uint32_t)std::min<uint64_t>(items, 1u << 30);
-}
-
-// MCCS_DIRECT_BLOCKS: most workgroups per rank of a direct launch (default 128).
+// MCCS_DIRECT_BLOCKS: most workgroups per rank of a direct launch (default
+// 128; read per launch: sweeps switch it).
 static int direct_max_blocks() {
-  static const int v = [] {
-    const char* e = std::getenv("MCCS_DIRECT_BLOCKS");
-    const int x = e ? std::atoi(e) : 0;
-    return x > 0 ? x : 128;
-  }();
-  return v;
+  const char* e = std::getenv("MCCS_DIRECT_BLOCKS");
+  const int x = e ? std::atoi(e) : 0;
+  return x > 0 ? x : 128;
 }
 
 // Every comm of the device group holds one direct AllReduce of the same shape
@@ -434,7 +412,9 @@ static bool direct_group(std::vector<Comm*>& comms, const std::vector<int>& idx)
     if (!ck->plan_direct) return false;
     if (ck->nranks != c0->nranks || ck->direct.count != c0->direct.count || ck->plan_dtype != c0->plan_dtype ||
         ck->plan_op != c0->plan_op || ck->rings != c0->rings || ck->cfg.buffer_size != c0->cfg.buffer_size ||
-        ck->layout.direct_slot != c0->layout.direct_slot || ck->nch != c0->nch)
+        ck->layout.direct_slot != c0->layout.direct_slot || ck->layout.oneshot_slot != c0->layout.oneshot_slot ||
+        ck->cfg.oneshot_bytes != c0->cfg.oneshot_bytes || ck->cfg.direct_bytes != c0->cfg.direct_bytes ||
+        ck->nch != c0->nch)
       return false;
   }
   return idx.size() <= MCCS_MULTI_MAX_RANKS;
@@ -455,6 +435,10 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   const int n = c0->nranks;
   da->count = c0->direct.count;
   da->slot_bytes = c0->layout.direct_slot;
+  da->oslot_bytes = c0->layout.oneshot_slot;
+  const size_t nbytes = (size_t)c0->direct.count * esize;
+  const bool oneshot = c0->layout.oneshot_slot > 0 && nbytes <= (size_t)c0->cfg.oneshot_bytes;
+  da->mode = oneshot ? MCCS_DIRECT_ONE_SHOT : MCCS_DIRECT_TWO_SHOT;
   da->nranks = (uint32_t)n;
   da->nch = (uint32_t)chans.size();
   da->nthr_ref = (uint32_t)nthr;
@@ -486,9 +470,14 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
                             ? 0
                             : std::max(da->timeout_ticks, ck->kcfg.timeout_ticks);
   }
+  // Workgroups: ~8 KiB of phase-1 bytes each at least, at most
+  // MCCS_DIRECT_BLOCKS; pieces: each phase's bytes over the workgroups, in
+  // 4 KiB steps (aligned: chunk offsets are granule multiples), 4..64 KiB.
+  // One-shot: phase 1 sends the whole input, phase 2 reduces all of it.
+  const size_t bytes = nbytes;
+  const size_t scatter = oneshot ? bytes : bytes - bytes / n;  // two-shot phases 1 and 3: chunks others own
   const int cap = coresident_direct_blocks(c0->device);
-  long g = std::min<long>(direct_item_count(da->count, esize, n, (int)da->nch, nthr, (int)da->buff_size),
-                          direct_max_blocks());
+  long g = std::min<long>((long)((scatter + 8191) / 8192), direct_max_blocks());
   if (idx.size() > 1) g = std::min<long>(g, cap / (long)idx.size());  // one fused launch: co-scheduled
   else if (c0->share > 1) g = std::min<long>(g, cap / 2 / c0->share);  // separate processes: half the slots
   g = std::max<long>(g, 1);
@@ -498,6 +487,13 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
     return mccsInvalidUsage;
   }
   *grid_x = (unsigned)g;
+  auto piece = [&](size_t phase_bytes) {
+    size_t p = (phase_bytes + (size_t)g - 1) / (size_t)g;
+    p = std::min<size_t>(std::max<size_t>((p + 4095) & ~(size_t)4095, 4096), 65536);
+    return (uint32_t)(p / esize);
+  };
+  da->piece = piece(scatter);
+  da->piece2 = piece(oneshot ? bytes : bytes / n + 1);
   for (size_t k = 0; k < idx.size(); ++k) {
     Comm* ck = comms[idx[k]];
     ck->plan_direct = false;
@@ -633,7 +629,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
     for (size_t k = 0; k < idx.size(); ++k) {
       comms[idx[k]]->event_recorded = record;
-      comms[idx[k]]->last_algo = direct ? MCCS_ALGO_DIRECT : MCCS_ALGO_RING;
+      comms[idx[k]]->last_algo = !direct ? MCCS_ALGO_RING : da.mode == MCCS_DIRECT_ONE_SHOT ? MCCS_ALGO_ONESHOT
+                                                                                         : MCCS_ALGO_DIRECT;
     }
     c0->event_recorded = record || stop_on_launch;
   }

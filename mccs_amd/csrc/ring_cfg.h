@@ -102,40 +102,50 @@ struct mccsMultiLaunchArgs {
 static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must stay within 4 KiB");
 #endif
 
-// ---- Direct (two-shot) AllReduce on a fully connected node (direct_kernel.h)
+// ---- Direct AllReduce on a fully connected node (direct_kernel.h)
 // Every rank reaches every peer's arena over its own xGMI link, so instead of
-// 2(n-1) ring hops a bucket takes two: each rank writes every chunk it does
-// not own into the owner's "in" slots (all links at once), each owner
-// reduces its chunks in exactly the ring's order (all_reduce.h chunk
-// ownership and summation order, so results are bit-identical to the ring
-// and the oracle) and writes the result into every peer's "out" slot, and
-// every rank copies the results it does not own to its output.  Per-rank
-// link bytes 2(n-1)/n*S, as the ring's.  Used for buckets up to the
-// communicator's direct capacity (MCCS_DIRECT_MAX bytes).
+// 2(n-1) ring hops a bucket takes two (two-shot: each rank writes every chunk
+// it does not own into the owner's "in" slot, each owner reduces its chunks
+// in exactly the ring's order and writes the result into every peer's "out"
+// slot, every rank copies the results it does not own to its output) or one
+// (one-shot, small buckets: every rank writes its whole input into every
+// peer's one-shot slot and every rank reduces every chunk itself, in the
+// ring's order).  Chunk ownership and summation order are the ring's
+// (all_reduce.h), so results are bit-identical to the ring and the oracle.
 //
 // A rank's direct region (in its FIFO arena, after the ring's data):
 //   [control, MCCS_DIRECT_CTRL_BYTES]
-//   [in : MCCS_DIRECT_MAX_RANKS senders x slot_bytes]  (by element offset)
-//   [out: slot_bytes]
-// Launch seq s (1, 2, ...) is kept in the control block and advanced by the
-// last workgroup of every launch (graph replays keep counting); flags hold the
-// seq they announce and are waited on with >=.  One set of slots suffices:
-// a rank's in slots are refilled (phase 1 of launch s+1, which waits for
-// nothing) only by a peer that finished launch s, i.e. saw this rank's out
-// flag of s, posted after this rank's last read of its in slots; its out slot
-// is refilled (phase 2 of s+1) only by an owner that saw this rank's in flag
-// of s+1, posted after this rank finished launch s.  Counters are this rank's
-// own and reset by the workgroup that completes them, before the launch ends.
+//   [two-shot in : MCCS_DIRECT_MAX_RANKS senders x slot_bytes]  (by element offset)
+//   [two-shot out: slot_bytes]
+//   [one-shot in : 2 parities x MCCS_DIRECT_MAX_RANKS senders x oslot_bytes]
+// Hand-offs are element counts: a sender adds the elements it wrote into a
+// rank's slot to that rank's IN_CNT line (one remote atomic per workgroup and
+// target, after its stores drained), an owner adds the elements it broadcast
+// to every peer's OUT_CNT line.  Counts only grow; the receiver keeps running
+// totals of what it has been sent so far (E_IN, E_OUT) and waits for
+// total + this launch's share.  Launch seq s (1, 2, ...) is counted in the
+// control block by the last workgroup of every launch (graph replays keep
+// counting).  Reuse across back-to-back launches:
+//   two-shot slots: a rank's in slots are refilled (phase 1 of launch s+1,
+//     which waits for nothing) only by a peer that finished launch s, which
+//     needed this rank's broadcast of s (or this rank owned nothing and read
+//     no in slot); its out slot is refilled only by an owner that counted this
+//     rank's scatter of s+1, made after this rank finished launch s;
+//   one-shot slots alternate by parity s & 1: a peer writes parity p in
+//     launch s+2 only after finishing s+1, which needed this rank's writes of
+//     s+1, made after this rank finished reading parity p in launch s.
 #define MCCS_DIRECT_MAX_RANKS 8
 #define MCCS_DIRECT_CTRL_BYTES 65536
-#define MCCS_DIRECT_IN_FLAG(s) ((s) * MCCS_FLAG_LINE_BYTES)              // posted by sender s
-#define MCCS_DIRECT_OUT_FLAG(s) (1024 + (s) * MCCS_FLAG_LINE_BYTES)      // posted by owner s
-#define MCCS_DIRECT_CNT_IN(t) (2048 + (t) * MCCS_FLAG_LINE_BYTES)        // our workgroups done writing t's in slot
-#define MCCS_DIRECT_CNT_OUT(t) (3072 + (t) * MCCS_FLAG_LINE_BYTES)       // ... t's out slot
-#define MCCS_DIRECT_DONE 4096
-#define MCCS_DIRECT_LAUNCHES 4224
-#define MCCS_DIRECT_SLOTS (MCCS_DIRECT_MAX_RANKS + 1)
+#define MCCS_DIRECT_IN_CNT(s) ((s) * MCCS_FLAG_LINE_BYTES)             // u64, added to by sender s
+#define MCCS_DIRECT_OUT_CNT(o) (1024 + (o) * MCCS_FLAG_LINE_BYTES)     // u64, added to by owner o
+#define MCCS_DIRECT_E_IN 2048                                          // u64: elements each sender sent so far
+#define MCCS_DIRECT_E_OUT(o) (2048 + 64 + (o) * 8)                     // u64: elements owner o broadcast so far
+#define MCCS_DIRECT_DONE 4096                                          // u32: workgroups done with the launch
+#define MCCS_DIRECT_LAUNCHES 4224                                      // u64: launches completed
+#define MCCS_DIRECT_SLOTS (MCCS_DIRECT_MAX_RANKS + 1)                  // two-shot slots
 #define MCCS_DIRECT_THREADS 512
+#define MCCS_DIRECT_TWO_SHOT 0
+#define MCCS_DIRECT_ONE_SHOT 1
 
 struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
   const void* send;
@@ -148,11 +158,14 @@ struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
 struct mccsDirectArgs {
   struct mccsDirectRank r[MCCS_MULTI_MAX_RANKS];
   uint64_t count;          // elements
-  uint64_t slot_bytes;     // bytes of one in/out slot (>= count * element size)
+  uint64_t slot_bytes;     // bytes of one two-shot slot (>= count * element size for two-shot)
+  uint64_t oslot_bytes;    // bytes of one one-shot slot (>= count * element size for one-shot)
   uint64_t timeout_ticks;  // s_memrealtime ticks; 0 = never
   uint32_t nranks, nch, nthr_ref, buff_size;  // the ring walk this launch reproduces
   uint32_t fence_mode;                        // MCCS_FENCE_*
-  uint32_t pad;
+  uint32_t mode;                              // MCCS_DIRECT_TWO_SHOT / ONE_SHOT
+  uint32_t piece;                             // elements per piece of the scatter / gather phases
+  uint32_t piece2;                            // elements per piece of the reduction phase
   uint8_t idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];  // rank at ring index k of channel bid
 };
 #ifdef __cplusplus

@@ -1,12 +1,14 @@
-"""GPU parity of the direct (two-shot) AllReduce against the oracle.
+"""GPU parity of the direct AllReduce (two-shot and one-shot) against the oracle.
 
-The direct kernel (mccs_amd/csrc/direct_kernel.h) sends every ring chunk to
-its owner, reduces it there in the ring's order and broadcasts the result,
-so its output must equal the ring's -- and the oracle's ring-order
-restatement -- bit for bit, for the same channels, thread count and rings
-the planner would have given the ring (vnode.expected_allreduce).  Runs on
-the virtual node (all ranks on cuda:0, one fused launch); every test also
-asserts that the call really took the direct kernel (Communicator.last_algo).
+The direct kernel (mccs_amd/csrc/direct_kernel.h) either sends every ring
+chunk to its owner, reduces it there in the ring's order and broadcasts the
+result (two-shot), or sends every input everywhere and lets each rank reduce
+every chunk in the ring's order (one-shot), so its output must equal the
+ring's -- and the oracle's ring-order restatement -- bit for bit, for the
+same channels, thread count and rings the planner would have given the ring
+(vnode.expected_allreduce).  Runs on the virtual node (all ranks on cuda:0,
+one fused launch); every test also asserts that the call really took the
+variant under test (Communicator.last_algo).
 """
 import numpy as np
 import pytest
@@ -18,10 +20,12 @@ pytestmark = pytest.mark.gpu
 
 F16, F32, BF16, I32, F64, I8 = 6, 7, 9, 2, 8, 0
 DIRECT = 8 << 20
+VARIANTS = ["direct", "oneshot"]
 
 
-def _cfg(**kw):
-    kw.setdefault("direct_bytes", DIRECT)
+def _cfg(variant="direct", **kw):
+    kw.setdefault("direct_bytes", DIRECT if variant == "direct" else -1)
+    kw.setdefault("oneshot_bytes", DIRECT if variant == "oneshot" else -1)
     return C.CommConfig(**kw)
 
 
@@ -34,137 +38,152 @@ def _algo(comms, want="direct"):
     assert all(c.last_algo() == want for c in comms), [c.last_algo() for c in comms]
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("code", [F32, F16, BF16])
-def test_direct_matches_oracle(orc, n, code):
-    comms = C.init_all([0] * n, _cfg())
+def test_direct_matches_oracle(orc, n, code, variant):
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(n * 10 + code)
         inputs = [vnode.gen(code, 300007, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, code, 0)
-        _algo(comms)
+        _algo(comms, variant)
         _check(outs, vnode.expected_allreduce(orc, inputs, code, 0, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("code", list(range(10)))
 @pytest.mark.parametrize("op", [0, 1, 2, 3])
-def test_direct_every_dtype_and_op(orc, code, op):
+def test_direct_every_dtype_and_op(orc, code, op, variant):
     n = 4
-    comms = C.init_all([0] * n, _cfg())
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(code * 4 + op)
         inputs = [vnode.gen(code, 40013, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, code, op)
-        _algo(comms)
+        _algo(comms, variant)
         _check(outs, vnode.expected_allreduce(orc, inputs, code, op, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("count", [1, 7, 255, 4097, 16385, 65536 * 3 + 5, (2 << 20) - 1])
-def test_direct_sizes(orc, count):
+def test_direct_sizes(orc, count, variant):
     """Tiny buckets (fewer elements than chunks: some owners get none) up to
     the direct capacity (8 MiB of fp32)."""
     n = 8
-    comms = C.init_all([0] * n, _cfg())
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(count)
         inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, F32, 0)
-        _algo(comms)
+        _algo(comms, variant)
         _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("n", [3, 8])
-def test_direct_multi_loop_walk(orc, n):
+def test_direct_multi_loop_walk(orc, n, variant):
     """A small FIFO buffer (64 KiB: 8 KiB chunks) makes the ring walk several
     loops plus a partial one inside one direct bucket; the kernel's walk must
     follow (all_reduce.h loop / realChunkSize rounding)."""
     buff = 1 << 16
-    comms = C.init_all([0] * n, _cfg(buffer_size=buff))
+    comms = C.init_all([0] * n, _cfg(variant, buffer_size=buff))
     try:
         rng = np.random.default_rng(n)
         count = 3 * comms[0].nchannels * n * (buff // 8 // 2 * 4 // 2) + 12345
         inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, F16, 0)
-        _algo(comms)
+        _algo(comms, variant)
         _check(outs, vnode.expected_allreduce(orc, inputs, F16, 0, comms[0], buff_size=buff))
     finally:
         vnode.destroy(comms)
 
 
-def test_direct_doubled_channels_and_custom_rings(orc):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_direct_doubled_channels_and_custom_rings(orc, variant):
     n = 8
     rings = C.default_rings(8, 0)
     rings = rings + [list(reversed(r)) for r in rings]  # 14 channels
-    comms = C.init_all([0] * n, _cfg(rings=rings))
+    comms = C.init_all([0] * n, _cfg(variant, rings=rings))
     try:
         assert comms[0].nchannels == 14
         rng = np.random.default_rng(5)
         inputs = [vnode.gen(BF16, 777777, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, BF16, 0)
-        _algo(comms)
+        _algo(comms, variant)
         _check(outs, vnode.expected_allreduce(orc, inputs, BF16, 0, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
-def test_direct_in_place(orc):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_direct_in_place(orc, variant):
     n = 4
-    comms = C.init_all([0] * n, _cfg())
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(11)
         inputs = [vnode.gen(F32, 500001, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, F32, 0, inplace=True)
-        _algo(comms)
+        _algo(comms, variant)
         _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
 def test_direct_and_ring_interleaved(orc):
-    """Buckets on either side of the threshold alternate on the same comms:
-    the direct launches' sequence counter and the ring's FIFO steps both stay
-    in lock-step, every result exact."""
+    """Buckets on every side of the thresholds alternate on the same comms:
+    the direct launches' running counts, the one-shot parity and the ring's
+    FIFO steps all stay in lock-step, every result exact."""
     n = 4
-    comms = C.init_all([0] * n, _cfg(direct_bytes=1 << 20))
+    comms = C.init_all([0] * n, C.CommConfig(direct_bytes=1 << 20, oneshot_bytes=64 << 10))
     try:
         rng = np.random.default_rng(3)
-        for it, count in enumerate([1000, 300000, 262144, 262145, 5, 1 << 20, 77777] * 2):
+        for it, count in enumerate([1000, 300000, 262144, 16384, 16385, 262145, 5, 1 << 20, 77777, 3, 4] * 2):
             inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
             outs = vnode.run_allreduce(comms, inputs, F32, 0)
-            _algo(comms, "direct" if count * 4 <= (1 << 20) else "ring")
+            nb = count * 4
+            _algo(comms, "oneshot" if nb <= 64 << 10 else "direct" if nb <= (1 << 20) else "ring")
             _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
-def test_direct_many_back_to_back(orc):
-    """200 launches without a sync in between (flags are sequence numbers in
-    one set of slots: ring_cfg.h's argument for back-to-back launches)."""
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_direct_many_back_to_back(orc, variant):
+    """Launches without a sync in between, each with its own inputs and
+    output (ring_cfg.h's argument for reusing the slots of back-to-back
+    launches: a slot overwritten too early shows up as a wrong result), then
+    200 more of the same call."""
     import torch
 
-    n, count = 8, 65537
-    comms = C.init_all([0] * n, _cfg())
+    n, count, k = 8, 65537, 24
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(8)
-        inputs = [vnode.gen(F32, count, rng, dist="exact") for _ in range(n)]
-        send = [vnode.to_dev(x) for x in inputs]
-        recv = [vnode.to_dev(np.zeros_like(x)) for x in inputs]
+        inputs = [[vnode.gen(F32, count, rng) for _ in range(n)] for _ in range(k)]
+        send = [[vnode.to_dev(x) for x in inp] for inp in inputs]
+        recv = [[vnode.to_dev(np.zeros_like(x)) for x in inp] for inp in inputs]
+        for i in range(k):
+            with C.group():
+                for r in range(n):
+                    C.all_reduce(comms[r], send[i][r], recv[i][r], count, F32, 0)
         for _ in range(200):
             with C.group():
                 for r in range(n):
-                    C.all_reduce(comms[r], send[r], recv[r], count, F32, 0)
+                    C.all_reduce(comms[r], send[0][r], recv[0][r], count, F32, 0)
         torch.cuda.synchronize()
         for c in comms:
             c.sync()
-        _algo(comms)
-        exp = vnode.expected_allreduce(orc, inputs, F32, 0, comms[0])
-        _check([vnode.from_dev(recv[r], F32) for r in range(n)], exp)
+        _algo(comms, variant)
+        for i in range(k):
+            exp = vnode.expected_allreduce(orc, inputs[i], F32, 0, comms[0])
+            _check([vnode.from_dev(recv[i][r], F32) for r in range(n)], exp)
     finally:
         vnode.destroy(comms)
 
@@ -199,14 +218,15 @@ def test_direct_group_of_two_takes_the_ring(orc):
         vnode.destroy(comms)
 
 
-def test_direct_captured_in_hip_graph(orc):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_direct_captured_in_hip_graph(orc, variant):
     """Direct launches captured into a HIP graph replay with fresh inputs,
     interleaved with eager direct calls (the launch counter lives in device
     memory, so replays and eager launches keep counting together)."""
     import torch
 
     n, count = 4, 123457
-    comms = C.init_all([0] * n, _cfg())
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(13)
         send = [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)]
@@ -236,7 +256,7 @@ def test_direct_captured_in_hip_graph(orc):
             torch.cuda.synchronize()
             for c in comms:
                 c.sync()
-            _algo(comms)
+            _algo(comms, variant)
             exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0])
             _check([recv[r].cpu().numpy() for r in range(n)], exp)
     finally:
@@ -244,12 +264,13 @@ def test_direct_captured_in_hip_graph(orc):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("code,off", [(F16, 2), (F32, 12)])
-def test_direct_misaligned_buffers(orc, code, off):
+def test_direct_misaligned_buffers(orc, code, off, variant):
     import torch
 
     n, count = 3, 100003
-    comms = C.init_all([0] * n, _cfg())
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(off)
         inputs = [vnode.gen(code, count, rng) for _ in range(n)]
@@ -263,25 +284,26 @@ def test_direct_misaligned_buffers(orc, code, off):
                 C.all_reduce(comms[r], sbuf[r].data_ptr() + off, rbuf[r].data_ptr() + off, count, code, 0)
         for c in comms:
             c.sync()
-        _algo(comms)
+        _algo(comms, variant)
         outs = [rbuf[r][off:off + nbytes].cpu().numpy().view(inputs[0].dtype) for r in range(n)]
         _check(outs, vnode.expected_allreduce(orc, inputs, code, 0, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("fifo", [C.FIFO_DEVICE, C.FIFO_UNCACHED_RELEASE])
-def test_direct_hand_off_modes(orc, fifo):
+def test_direct_hand_off_modes(orc, fifo, variant):
     """Cached arena (system-scope release before counting out, acquire after
     a wait) and uncached + release fence."""
     n = 4
-    comms = C.init_all([0] * n, _cfg(fifo_memory=fifo))
+    comms = C.init_all([0] * n, _cfg(variant, fifo_memory=fifo))
     try:
         rng = np.random.default_rng(fifo)
         for count in (70001, 1 << 20):
             inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
             outs = vnode.run_allreduce(comms, inputs, F32, 0)
-            _algo(comms)
+            _algo(comms, variant)
             _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
