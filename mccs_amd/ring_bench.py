@@ -372,6 +372,68 @@ def size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20, graph_upt
     return rows
 
 
+def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, ring_rows, upto=8 << 20,
+                 oneshot_upto=2 << 20, warmup=3, K=20):
+    """The direct AllReduce variants (direct_kernel.h) beside the ring over the
+    sweep's sizes up to `upto`: two-shot and one-shot communicators built with
+    the measured transport's config, every size exact-sum validated, eager
+    and graph-replayed latency per call (max over ranks).  ring_rows: the
+    size sweep's rows of the ring.  Ends with the thresholds the table
+    supports (the largest size each variant still beats the ring)."""
+    import dataclasses
+
+    out = {"sizes": [nb for nb in SWEEP_BYTES if nb <= upto], "rows": []}
+    ring = {r["bytes"]: r for r in ring_rows}
+    comms = {}
+    try:
+        for algo, kw in (("direct", dict(direct_bytes=upto, oneshot_bytes=-1)),
+                         ("oneshot", dict(direct_bytes=-1, oneshot_bytes=oneshot_upto))):
+            cfg = dataclasses.replace(config or C.CommConfig(), **kw)
+            comms[algo] = C.init_communicator_rank(rank, world, device, exchange, cfg)
+        for nb in out["sizes"]:
+            n = nb // 2
+            x = torch.empty(n, dtype=torch.float16, device=dev).uniform_(-1, 1)
+            y = torch.empty_like(x)
+            row = {"bytes": nb}
+            if nb in ring:
+                row["ring_us"] = ring[nb]["latency_us"]
+                if "graph_latency_us" in ring[nb]:
+                    row["ring_graph_us"] = ring[nb]["graph_latency_us"]
+            for algo, cm in comms.items():
+                if algo == "oneshot" and nb > oneshot_upto:
+                    continue
+
+                def step(cm=cm):
+                    C.all_reduce(cm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum)
+
+                el = max_over_ranks(dist, time_steps(torch, dist, cm, step, warmup, K)) / K
+                require(dist, cm.last_algo() == algo, f"{algo} sweep {nb} B took {cm.last_algo()}")
+                gl = graph_replay(torch, dist, cm, lambda st, cm=cm: C.all_reduce(
+                    cm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum, st), calls=10)
+                require(dist, exact_sum_ok(torch, C, cm, rank, world, n, torch.float16,
+                                           C.AllReduceDataType.Float16, dev), f"{algo} sweep {nb} B")
+                row[f"{algo}_us"] = round(el * 1e6, 2)
+                row[f"{algo}_graph_us"] = round(gl * 1e6, 2)
+            out["rows"].append(row)
+            del x, y
+        best = {}
+        for algo in ("direct", "oneshot"):
+            wins = [r["bytes"] for r in out["rows"] if f"{algo}_graph_us" in r and "ring_graph_us" in r
+                    and r[f"{algo}_graph_us"] < r["ring_graph_us"]]
+            best[f"{algo}_beats_ring_upto_bytes"] = max(wins) if wins else 0
+        out["summary"] = best
+    except BenchFailure:
+        raise
+    except Exception as e:  # noqa: BLE001  (informational leg: recorded, never fatal)
+        out["error"] = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        torch.cuda.synchronize()
+        for cm in comms.values():
+            cm.destroy()
+        dist.barrier()
+    return out
+
+
 def out_links(rings, rank):
     """Distinct xGMI links this rank sends on (one per distinct ring successor)."""
     nxt = set()
@@ -605,6 +667,9 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
         extras["allgather_16MiB_per_rank"] = extra_allgather(torch, dist, C, comm, rank, world, dev)
         extras["size_sweep_fp16"] = size_sweep(torch, dist, C, comm, rank, world, dev)
     info = {"channels": comm.nchannels, "lanes": comm.lanes, "block_threads": comm.block_threads}
+    if not getattr(args, "no_extra", False) and "size_sweep_fp16" in extras and 2 <= world <= 8:
+        extras["direct_sweep_fp16"] = direct_sweep(torch, dist, C, rank, world, device, dev, exchange,
+                                                   mode_config(C, mode, info), extras["size_sweep_fp16"])
     rings = comm.rings()
     comm.destroy()
     if (not getattr(args, "no_extra", False) and world % 2 == 0

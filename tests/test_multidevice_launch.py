@@ -349,3 +349,30 @@ def test_direct_off_by_default_and_fused_ranks(fake):
     finally:
         for c in comms + (plain or []):
             c.destroy()
+
+
+def test_oneshot_below_its_threshold(fake):
+    """Buckets up to oneshot_bytes take the one-shot variant, larger ones up
+    to direct_bytes the two-shot one, the rest the ring; pieces stay within
+    4..64 KiB."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(direct_bytes=4 << 20, oneshot_bytes=256 << 10))
+    try:
+        for count, want, mode in ((1000, "oneshot", "oneshot"), (65536, "oneshot", "oneshot"),
+                                  (65537, "direct", "twoshot"), (1 << 20, "direct", "twoshot"),
+                                  ((1 << 20) + 1, "ring", None)):
+            _log()
+            _allreduce_group(comms, count=count)
+            launches = [kv for k, kv in _log() if k == "launch"]
+            assert len(launches) == 8
+            assert all(c.last_algo() == want for c in comms), (count, [c.last_algo() for c in comms])
+            if mode:
+                for kv in launches:
+                    assert kv["kind"] == "direct" and kv["mode"] == mode
+                    for p in (int(kv["piece"]), int(kv["piece2"])):
+                        assert 1024 <= p <= 16384  # fp32 elements: 4..64 KiB
+        for c in comms:
+            c.sync()
+    finally:
+        for c in comms:
+            c.destroy()
