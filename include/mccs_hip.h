@@ -192,6 +192,11 @@ mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int *order);
 #define MCCS_ALGO_DIRECT 1
 #define MCCS_ALGO_ONESHOT 2
 int mccsCommLastAlgo(mccsComm_t comm);
+/* 1 when the comm may run the direct kernel: a direct region was configured
+ * and every device of the communicator can perform atomics on every other's
+ * memory (hipDevP2PAttrNativeAtomicSupported; the hand-off counts are remote
+ * atomics).  Otherwise every AllReduce takes the ring. */
+int mccsCommDirectEnabled(mccsComm_t comm);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
 const char *mccsGetErrorString(mccsResult_t r);

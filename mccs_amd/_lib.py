@@ -107,6 +107,7 @@ SIGNATURES: dict[str, tuple] = {
     "mccsCommRing": (_c_int, [_c_void_p, _c_int, _P(_c_int)]),
     "mccsCommDevComm": (_c_int, [_c_void_p, _P(_c_void_p)]),
     "mccsCommLastAlgo": (_c_int, [_c_void_p]),
+    "mccsCommDirectEnabled": (_c_int, [_c_void_p]),
     "mccs_ring_profile": (_c_int, [_c_int, _P(ctypes.c_ulonglong), _c_int]),
     "mccsMemAllocShared": (_c_int, [_c_int, _c_size_t, _P(_c_void_p), _c_void_p]),
     "mccsMemFreeShared": (_c_int, [_c_int, _c_void_p]),

@@ -151,6 +151,11 @@ class Communicator:
         a = _sig().mccsCommLastAlgo(self._h)
         return {0: "ring", 1: "direct", 2: "oneshot"}.get(a)
 
+    def direct_enabled(self) -> bool:
+        """Whether AllReduces may take the direct kernel (a direct region is
+        configured and every device pair supports peer atomics)."""
+        return bool(_sig().mccsCommDirectEnabled(self._h))
+
     def dev_comm(self) -> int:
         p = ctypes.c_void_p()
         _lib.check(_sig().mccsCommDevComm(self._h, ctypes.byref(p)), "mccsCommDevComm")

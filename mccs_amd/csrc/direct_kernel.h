@@ -256,6 +256,16 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
     }
     direct_chunks(w, a, [&](int64_t, int64_t ne, int, int, uint32_t owner) { sh.owned[owner] += (uint64_t)ne; });
   }
+  // Arrival: once every workgroup of the launch has read the start values
+  // above, the last to arrive may advance them for the next launch.  The
+  // count is issued now and its result consumed after phase 1 (its round
+  // trip overlaps the scatter); the loads above complete first.
+  uint32_t arrived = 0;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    arrived = __hip_atomic_fetch_add((uint32_t*)(mine + MCCS_DIRECT_DONE), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   const uint64_t seq = sh.seq;
   const int64_t esz = (int64_t)sizeof(T);
@@ -265,6 +275,21 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   const int64_t piece2 = a.piece2 > 0 ? (int64_t)a.piece2 : 1;
   u32x4 nopre[1];
   __shared__ uint64_t need[MCCS_DIRECT_MAX_RANKS];
+  // The last workgroup to arrive advances the running totals and the launch
+  // count for the next launch (every workgroup of this one has its copies).
+  auto advance = [&]() {
+    if (threadIdx.x == 0 && arrived + 1 == G) {
+      __hip_atomic_store((uint32_t*)(mine + MCCS_DIRECT_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_IN),
+                         sh.e_in + (one_shot ? (uint64_t)w.size : sh.owned[me.rank]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (!one_shot)
+        for (int t = 0; t < n; ++t)
+          __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_OUT(t)), sh.e_out[t] + sh.owned[t], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_LAUNCHES), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
 
   if (one_shot) {
     const int64_t oslot = (int64_t)a.oslot_bytes;
@@ -284,6 +309,7 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
         for (int t = 0; t < n; ++t) sh.sent[t] += (uint64_t)ne;
     }
     direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
+    advance();
     // 2. every chunk, reduced in the ring's order into the output
     if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + (uint64_t)w.size;
     __syncthreads();
@@ -330,6 +356,7 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
       if (threadIdx.x == 0) sh.sent[owner] += (uint64_t)ne;
     });
     direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
+    advance();
 
     // 2. reduce the chunks this rank owns, in the ring's order; broadcast
     if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + sh.owned[me.rank];
@@ -378,24 +405,6 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
     });
   }
 
-  // the launch is over for this workgroup: the last one advances the running
-  // totals and the launch count (read by the next launch, after this one)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0 && sh.ok) {
-    uint32_t* done = (uint32_t*)(mine + MCCS_DIRECT_DONE);
-    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == G) {
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_IN),
-                         sh.e_in + (one_shot ? (uint64_t)w.size : sh.owned[me.rank]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      if (!one_shot)
-        for (int t = 0; t < n; ++t)
-          __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_OUT(t)), sh.e_out[t] + sh.owned[t], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_LAUNCHES), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 template <int DT, int OP>

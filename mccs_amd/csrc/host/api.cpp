@@ -32,10 +32,15 @@ static void group_discard() {
   g_group.streams.clear();
 }
 
-// Direct AllReduce threshold when the config leaves it 0 (MCCS_DIRECT_BYTES
-// overrides): buckets up to this many bytes per rank take the two-shot kernel.
-static constexpr int kDirectDefaultBytes = 0;
-static constexpr int kOneshotDefaultBytes = 0;  // MCCS_ONESHOT_BYTES
+// Direct AllReduce thresholds when the config leaves them 0 (MCCS_DIRECT_BYTES /
+// MCCS_ONESHOT_BYTES override): buckets up to this many bytes per rank take
+// the two-shot / one-shot kernel (bit-identical to the ring either way).
+// One-shot to 256 KiB: it beat the ring on the virtual node up to 512 KiB at
+// n = 8 and 2 MiB at n <= 4 (profiles/r03_direct_vnode.json), and over xGMI
+// the ring's 2(n-1) sequential hops only cost more.  Two-shot stays off
+// until the node's sweep (bench config.direct_sweep_fp16) shows where it wins.
+static constexpr int kDirectDefaultBytes = -1;
+static constexpr int kOneshotDefaultBytes = 256 << 10;
 
 static void fill_defaults(mccsCommConfig* c) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
@@ -235,10 +240,12 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
       all_uc = all_uc && cs[i]->own_arena_uncached;
       release = release || cs[i]->cfg.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
     }
+    const bool atomics = devices_p2p_atomics(std::vector<int>(devices, devices + nranks));
     for (int i = 0; i < nranks; ++i) {
       for (int j = 0; j < nranks; ++j) cs[i]->peer_arena[j] = cs[j]->own_arena;
       cs[i]->all_uncached = all_uc;
       cs[i]->fifo_release = release;
+      cs[i]->direct_ok = atomics;
     }
     for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_build_device(cs[i]);
   }
@@ -362,6 +369,11 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
   }
   c->all_uncached = all_uc;
   c->fifo_release = release;
+  {
+    std::vector<int> devs;
+    for (int r = 0; r < c->nranks; ++r) devs.push_back(hs[r].device);
+    c->direct_ok = devices_p2p_atomics(devs);
+  }
   return comm_build_device(c);
 }
 
@@ -456,6 +468,11 @@ extern "C" mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int* order) {
 extern "C" int mccsCommLastAlgo(mccsComm_t comm) {
   const Comm* c = (const Comm*)comm;
   return c ? c->last_algo : -1;
+}
+
+extern "C" int mccsCommDirectEnabled(mccsComm_t comm) {
+  const Comm* c = (const Comm*)comm;
+  return c && c->direct_ok && (c->layout.direct_slot > 0 || c->layout.oneshot_slot > 0);
 }
 
 extern "C" mccsResult_t mccsCommDevComm(mccsComm_t comm, void** dev_comm) {

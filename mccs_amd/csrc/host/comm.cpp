@@ -102,6 +102,18 @@ void default_rings(int n, int nch_req, std::vector<std::vector<int>>* rings) {
 }
 
 // ---------------------------------------------------------------------------
+bool devices_p2p_atomics(const std::vector<int>& devices) {
+  for (int a : devices)
+    for (int b : devices) {
+      int ok = 0;
+      if (rt().P2PAtomics(&ok, a, b) != hipSuccess || !ok) {
+        (void)hipGetLastError();
+        return false;
+      }
+    }
+  return true;
+}
+
 mccsResult_t comm_set_kernel_cfg(Comm* c) {
   mccsRingKernelCfg k{};
   k.fence_mode = !c->all_uncached ? MCCS_FENCE_SYSTEM : c->fifo_release ? MCCS_FENCE_UNCACHED_RELEASE : MCCS_FENCE_UNCACHED;

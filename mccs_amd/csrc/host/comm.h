@@ -182,10 +182,15 @@ struct Comm {
     size_t count;
   } direct{};
   int share = 1;         // ranks of this communicator on this rank's GPU (co-residency of spinning launches)
+  // Every device of the communicator can perform atomics on every other's
+  // memory (the direct kernel's hand-off counts are remote atomics); all ranks
+  // derive it from the same device set, so they agree.
+  bool direct_ok = false;
   int last_algo = -1;    // MCCS_ALGO_* of the latest launch
 };
 
 // comm.cpp
+bool devices_p2p_atomics(const std::vector<int>& devices);
 mccsResult_t comm_alloc_local(Comm* c);
 mccsResult_t comm_switch_to_device_arena(Comm* c);
 mccsResult_t comm_build_device(Comm* c);

@@ -120,7 +120,7 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   const size_t bytes = count * (size_t)elem_bytes(dtype);
   const bool oneshot = c->layout.oneshot_slot > 0 && bytes <= (size_t)c->cfg.oneshot_bytes;
   const bool twoshot = c->layout.direct_slot > 0 && bytes <= (size_t)c->cfg.direct_bytes;
-  if (!c->plan_pending && func == mccsFuncAllReduce && (oneshot || twoshot)) {
+  if (!c->plan_pending && func == mccsFuncAllReduce && c->direct_ok && (oneshot || twoshot)) {
     c->plan_direct = true;
     c->direct.send = send;
     c->direct.recv = recv;

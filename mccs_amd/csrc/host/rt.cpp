@@ -50,6 +50,13 @@ class HipRuntime final : public DeviceRuntime {
   hipError_t DeviceSynchronize() override { return hipDeviceSynchronize(); }
   hipError_t FlushCaches() override { return ring_flush_caches(nullptr); }
   hipError_t CanAccessPeer(int* can, int dev, int peer) override { return hipDeviceCanAccessPeer(can, dev, peer); }
+  hipError_t P2PAtomics(int* ok, int dev, int peer) override {
+    if (dev == peer) {
+      *ok = 1;
+      return hipSuccess;
+    }
+    return hipDeviceGetP2PAttribute(ok, hipDevP2PAttrNativeAtomicSupported, dev, peer);
+  }
   hipError_t EnablePeerAccess(int peer) override {
     hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
     if (e == hipErrorPeerAccessAlreadyEnabled) e = hipSuccess;
@@ -164,6 +171,10 @@ class FakeRuntime final : public DeviceRuntime {
   }
   hipError_t EnablePeerAccess(int peer) override {
     note("peer dev=" + std::to_string(cur_) + " peer=" + std::to_string(peer));
+    return hipSuccess;
+  }
+  hipError_t P2PAtomics(int* ok, int dev, int peer) override {
+    *ok = dev >= 0 && dev < ndev_ && peer >= 0 && peer < ndev_ && !std::getenv("MCCS_TEST_NO_P2P_ATOMICS");
     return hipSuccess;
   }
   hipError_t EventCreate(hipEvent_t* e, unsigned) override {

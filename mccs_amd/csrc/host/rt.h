@@ -33,6 +33,8 @@ class DeviceRuntime {
   virtual hipError_t FlushCaches() = 0;  // ring_flush_caches on the null stream of the current device
   virtual hipError_t CanAccessPeer(int* can, int dev, int peer) = 0;
   virtual hipError_t EnablePeerAccess(int peer) = 0;  // from the current device; already-enabled is success
+  // Whether `dev` can perform atomics on `peer`'s memory (same device: yes).
+  virtual hipError_t P2PAtomics(int* ok, int dev, int peer) = 0;
   virtual hipError_t EventCreate(hipEvent_t* e, unsigned flags) = 0;
   virtual hipError_t EventDestroy(hipEvent_t e) = 0;
   virtual hipError_t EventRecord(hipEvent_t e, hipStream_t s) = 0;

@@ -123,9 +123,9 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 // target, after its stores drained), an owner adds the elements it broadcast
 // to every peer's OUT_CNT line.  Counts only grow; the receiver keeps running
 // totals of what it has been sent so far (E_IN, E_OUT) and waits for
-// total + this launch's share.  Launch seq s (1, 2, ...) is counted in the
-// control block by the last workgroup of every launch (graph replays keep
-// counting).  Reuse across back-to-back launches:
+// total + this launch's share.  Launch seq s (1, 2, ...) and the totals are
+// advanced in the control block by the last workgroup of a launch to arrive
+// (after every workgroup read them), so graph replays keep counting.  Reuse across back-to-back launches:
 //   two-shot slots: a rank's in slots are refilled (phase 1 of launch s+1,
 //     which waits for nothing) only by a peer that finished launch s, which
 //     needed this rank's broadcast of s (or this rank owned nothing and read
@@ -140,7 +140,7 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 #define MCCS_DIRECT_OUT_CNT(o) (1024 + (o) * MCCS_FLAG_LINE_BYTES)     // u64, added to by owner o
 #define MCCS_DIRECT_E_IN 2048                                          // u64: elements each sender sent so far
 #define MCCS_DIRECT_E_OUT(o) (2048 + 64 + (o) * 8)                     // u64: elements owner o broadcast so far
-#define MCCS_DIRECT_DONE 4096                                          // u32: workgroups done with the launch
+#define MCCS_DIRECT_DONE 4096                                          // u32: workgroups arrived in the launch
 #define MCCS_DIRECT_LAUNCHES 4224                                      // u64: launches completed
 #define MCCS_DIRECT_SLOTS (MCCS_DIRECT_MAX_RANKS + 1)                  // two-shot slots
 #define MCCS_DIRECT_THREADS 512

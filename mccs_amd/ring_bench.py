@@ -131,7 +131,9 @@ def _candidates(C, lanes_opts, locs, chan_opts=(None,)):
                     continue
                 # a correct 128 MiB AllReduce takes milliseconds: a mode whose hand-off
                 # fails over this node's links is caught by the watchdog within 20 s
-                kw = dict(locality=loc, lanes=lanes, timeout_ms=20000)
+                # the ring at every size (the library's one-shot default would take
+                # the sweep's small buckets; direct_sweep times those variants)
+                kw = dict(locality=loc, lanes=lanes, timeout_ms=20000, direct_bytes=-1, oneshot_bytes=-1)
                 if nch:
                     kw["channel_count"] = nch
                 tag = f"{lname}/lanes={lanes or 'auto'}" + (f"/channels={nch}" if nch else "")
@@ -739,7 +741,7 @@ def mode_config(C, mode: str, info: dict):
     fifo = {"uncached-fifo": C.FIFO_UNCACHED, "uncached-fifo+release-fence": C.FIFO_UNCACHED_RELEASE,
             "cached-fifo+system-fences": C.FIFO_DEVICE}.get(kind, C.FIFO_UNCACHED)
     return C.CommConfig(channel_count=info.get("channels"), lanes=info.get("lanes"), locality=loc, fifo_memory=fifo,
-                        timeout_ms=20000)
+                        timeout_ms=20000, direct_bytes=-1, oneshot_bytes=-1)
 
 
 def node_legs(torch, C, world, ndev, nbytes, config=None):

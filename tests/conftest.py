@@ -31,6 +31,16 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
+@pytest.fixture(autouse=True)
+def _ring_unless_direct(request, monkeypatch):
+    """Every test runs the ring at every size (the library's one-shot default
+    would otherwise take small buckets) unless its module sets
+    DIRECT_DEFAULTS = True (the direct kernel's own tests)."""
+    if not getattr(request.module, "DIRECT_DEFAULTS", False):
+        monkeypatch.setenv("MCCS_ONESHOT_BYTES", "-1")
+        monkeypatch.setenv("MCCS_DIRECT_BYTES", "-1")
+
+
 @pytest.fixture(scope="session")
 def orc():
     from oracle import oracle

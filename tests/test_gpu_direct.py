@@ -17,6 +17,7 @@ from mccs_amd import comm as C
 import vnode
 
 pytestmark = pytest.mark.gpu
+DIRECT_DEFAULTS = True  # conftest: keep the library's direct thresholds
 
 F16, F32, BF16, I32, F64, I8 = 6, 7, 9, 2, 8, 0
 DIRECT = 8 << 20
@@ -304,6 +305,23 @@ def test_direct_hand_off_modes(orc, fifo, variant):
             inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
             outs = vnode.run_allreduce(comms, inputs, F32, 0)
             _algo(comms, variant)
+            _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
+    finally:
+        vnode.destroy(comms)
+
+
+def test_library_defaults(orc):
+    """The library default: one-shot up to 256 KiB per rank, the ring above
+    (two-shot off until a node's sweep says where it wins)."""
+    n = 4
+    comms = C.init_all([0] * n)
+    try:
+        assert all(c.direct_enabled() for c in comms)
+        rng = np.random.default_rng(44)
+        for count, want in ((1000, "oneshot"), (65536, "oneshot"), (65537, "ring")):
+            inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
+            outs = vnode.run_allreduce(comms, inputs, F32, 0)
+            _algo(comms, want)
             _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)

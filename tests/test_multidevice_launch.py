@@ -20,6 +20,7 @@ from mccs_amd import _lib
 from mccs_amd import comm as C
 
 F32, SUM = 7, 0
+DIRECT_DEFAULTS = True  # conftest: these tests set the direct thresholds themselves
 
 
 def _parse(line):
@@ -328,10 +329,15 @@ def test_direct_allreduce_plans(fake):
             c.destroy()
 
 
-def test_direct_off_by_default_and_fused_ranks(fake):
+def test_direct_defaults_and_fused_ranks(fake, monkeypatch):
+    """Library defaults: one-shot up to 256 KiB, the ring above (two-shot
+    off); fused ranks on one device share one direct launch; without peer
+    atomics every AllReduce takes the ring."""
+    for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES"):
+        monkeypatch.delenv(k, raising=False)
     fake(2)
     comms = C.init_all([0, 0, 0, 0, 1, 1, 1, 1], C.CommConfig(direct_bytes=1 << 20))
-    plain = None
+    plain = none = None
     try:
         _log()
         _allreduce_group(comms, count=1000)
@@ -340,14 +346,26 @@ def test_direct_off_by_default_and_fused_ranks(fake):
         assert all(kv["grid"].endswith("x4") and kv["comms_on_dev"] == "1" for kv in launches)
         for c in comms:
             c.sync()
-        plain = C.init_all([0, 1])  # library default: no direct region, ring only
-        _log()
-        _allreduce_group(plain, count=1000)
-        assert [kv["kind"] for k, kv in _log() if k == "launch"] == ["ring"] * 2
+        plain = C.init_all([0, 1])
+        assert all(c.direct_enabled() for c in plain)
+        for count, want in ((1000, "oneshot"), (65536, "oneshot"), (65537, "ring")):
+            _log()
+            _allreduce_group(plain, count=count)
+            assert [kv["kind"] for k, kv in _log() if k == "launch"] == (["direct"] * 2 if want != "ring" else
+                                                                         ["ring"] * 2)
+            assert [c.last_algo() for c in plain] == [want] * 2
         for c in plain:
             c.sync()
+        monkeypatch.setenv("MCCS_TEST_NO_P2P_ATOMICS", "1")
+        none = C.init_all([0, 1])
+        assert not any(c.direct_enabled() for c in none)
+        _log()
+        _allreduce_group(none, count=1000)
+        assert [kv["kind"] for k, kv in _log() if k == "launch"] == ["ring"] * 2
+        for c in none:
+            c.sync()
     finally:
-        for c in comms + (plain or []):
+        for c in comms + (plain or []) + (none or []):
             c.destroy()
 
 
