@@ -32,3 +32,24 @@ const void* direct_kernel_ptr(int dtype, int op) {
 }
 
 }  // namespace mccs
+
+// Phase timeline of the latest direct launch (-DMCCS_DIRECT_TRACE builds,
+// tools/direct_trace.py): out[slot * kDtEvents + event] = s_memrealtime of workgroup
+// 0 of rank slot `slot` (direct_kernel.h kDt*); cleared after reading.
+// Returns the words written, or -1 when this build has no trace.
+extern "C" int mccs_direct_trace(unsigned long long* out, int max_words) {
+#ifdef MCCS_DIRECT_TRACE
+  constexpr int kWords = MCCS_MULTI_MAX_RANKS * mccs::kDtEvents;
+  if (max_words < kWords) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mccs::g_dtrace), sizeof(unsigned long long) * kWords, 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  static unsigned long long zero[kWords];
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(mccs::g_dtrace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+  return kWords;
+#else
+  (void)out;
+  (void)max_words;
+  return -1;
+#endif
+}

@@ -48,62 +48,87 @@ namespace mccs {
 
 constexpr int kDirectUnroll = 2;  // packs per lane per source in flight (x up to 8 sources)
 
+// Phase timeline of workgroup 0 of every rank slot (A/B builds only:
+// -DMCCS_DIRECT_TRACE, read with mccs_direct_trace; tools/direct_trace.py):
+// s_memrealtime (100 MHz) stored with plain vector stores, last launch wins.
+enum : int {
+  kDtStart = 0, kDtPhase1 = 1, kDtCounted1 = 2, kDtWait2 = 3, kDtPhase2 = 4, kDtCounted2 = 5, kDtWait3 = 6,
+  kDtEnd = 7, kDtPrologue = 8, kDtPiece1 = 9, kDtPiece3 = 10, kDtEvents = 12
+};
+#ifdef MCCS_DIRECT_TRACE
+namespace {
+__device__ unsigned long long g_dtrace[MCCS_MULTI_MAX_RANKS][kDtEvents];
+}  // namespace
+#define MCCS_DTRACE(ev)                                                                              \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_dtrace[blockIdx.y][ev] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define MCCS_DTRACE(ev) ((void)0)
+#endif
+
+// The walk in 32-bit arithmetic: a direct bucket holds < 2^31 elements
+// (direct_bytes <= 1 GiB), and 64-bit divisions are long software sequences
+// that a per-chunk loop run by every thread cannot afford.
 struct DirectWalk {
-  int64_t size, chunkSize, loopSize, gran;
-  int n, nch;
+  uint32_t size, chunkSize, loopSize, gran;
+  uint32_t n, nch;
 };
 
 template <int DT>
 __device__ __forceinline__ DirectWalk direct_walk(const mccsDirectArgs& a) {
   using T = typename Elem<DT>::T;
   DirectWalk w;
-  w.n = (int)a.nranks;
-  w.nch = (int)a.nch;
-  w.size = (int64_t)a.count;
+  w.n = a.nranks;
+  w.nch = a.nch;
+  w.size = (uint32_t)a.count;
   // all_reduce.h:17-21 with the ring kernel's arithmetic (ring_kernel.h run_elem)
-  const int64_t stepSize = (int64_t)((int)a.buff_size / MCCS_BUFFER_SLOTS / (int)sizeof(T));
-  w.chunkSize = (int64_t)(int)(stepSize * ALLREDUCE_CHUNKSTEPS);
-  w.loopSize = (int64_t)w.nch * w.n * w.chunkSize;
-  w.gran = (int64_t)((int)a.nthr_ref - WARP_SIZE) * 8 / (int64_t)sizeof(T);
+  const uint32_t stepSize = (uint32_t)((int)a.buff_size / MCCS_BUFFER_SLOTS / (int)sizeof(T));
+  w.chunkSize = stepSize * ALLREDUCE_CHUNKSTEPS;
+  const uint64_t loop = (uint64_t)w.nch * w.n * w.chunkSize;
+  w.loopSize = loop > 0x7fffffffu ? 0x7fffffffu : (uint32_t)loop;  // >= size: one loop
+  w.gran = ((a.nthr_ref - WARP_SIZE) * 8) / (uint32_t)sizeof(T);
   if (w.gran < 1) w.gran = 1;
   return w;
 }
 
-// Calls f(off, nelem, bid, k, owner) for every chunk of the ring's walk, in order.
-template <typename F>
-__device__ __forceinline__ void direct_chunks(const DirectWalk& w, const mccsDirectArgs& a, F&& f) {
-  for (int64_t g = 0; g < w.size; g += w.loopSize) {
-    int64_t rcs = div_up(w.size - g, (int64_t)w.nch * w.n);  // realChunkSize, all_reduce.h:30-36
+// This workgroup's pieces (pc elements) of the ring chunks `want(owner)`
+// selects, in walk order (all_reduce.h:28-42: loop, realChunkSize, chunk k
+// of channel bid at gridOffset + (bid*n + k)*realChunkSize): the selected
+// chunks' pieces are numbered 0, 1, ... and piece p goes to workgroup p % G.
+// Calls f(off, nelem, bid, k, owner).  Divisions: two per loop and one for
+// the walk's last, partial chunk; the piece numbering is kept mod G by
+// subtraction.
+template <typename W, typename F>
+__device__ __forceinline__ void direct_pieces(const DirectWalk& w, const uint8_t (*idx2rank)[MCCS_DIRECT_MAX_RANKS],
+                                              uint32_t pc, uint32_t G, uint32_t bx, W&& want, F&& f) {
+  uint32_t base = 0;  // (pieces of selected chunks before this one) mod G
+  const uint32_t parts = w.nch * w.n;
+  for (uint32_t g = 0; g < w.size; g += w.loopSize) {
+    uint32_t rcs = (w.size - g + parts - 1) / parts;  // realChunkSize, all_reduce.h:30-36
     rcs = w.chunkSize < rcs ? w.chunkSize : rcs;
-    rcs = (int64_t)(int)round_up(rcs, w.gran);
-    for (int bid = 0; bid < w.nch; ++bid)
-      for (int k = 0; k < w.n; ++k) {
-        const int64_t off = g + ((int64_t)bid * w.n + k) * rcs;
-        const int64_t ne = rcs < w.size - off ? rcs : w.size - off;
-        if (ne > 0) f(off, ne, bid, k, (uint32_t)a.idx2rank[bid][k]);
+    rcs = (rcs + w.gran - 1) / w.gran * w.gran;
+    const uint32_t np_full = (rcs + pc - 1) / pc;
+    for (uint32_t c = 0, bid = 0, k = 0; c < parts; ++c, k = k + 1 == w.n ? 0 : k + 1, bid += k == 0) {
+      const uint32_t off = g + c * rcs;
+      if (off >= w.size) return;  // every later chunk of the walk is empty
+      const uint32_t owner = idx2rank[bid][k];
+      if (!want(owner)) continue;
+      const uint32_t ne = rcs < w.size - off ? rcs : w.size - off;
+      const uint32_t np = ne == rcs ? np_full : (ne + pc - 1) / pc;
+      for (uint32_t j = bx >= base ? bx - base : bx + G - base; j < np; j += G) {
+        const uint32_t s = j * pc;
+        f((int64_t)(off + s), (int64_t)(ne - s < pc ? ne - s : pc), (int)bid, (int)k, owner);
       }
+      base += np;
+      while (base >= G) base -= G;
+    }
   }
 }
 
-// This workgroup's pieces (pc elements) of the chunks `want(owner)` selects:
-// the selected chunks' pieces are numbered 0, 1, ... in walk order and piece
-// p goes to workgroup p % G.  Calls f(off, nelem, bid, k, owner).
-template <typename W, typename F>
-__device__ __forceinline__ void direct_pieces(const DirectWalk& w, const mccsDirectArgs& a, int64_t pc, uint32_t G,
-                                              uint32_t bx, W&& want, F&& f) {
-  uint64_t base = 0;  // pieces of selected chunks before this one
-  direct_chunks(w, a, [&](int64_t off, int64_t ne, int bid, int k, uint32_t owner) {
-    if (!want(owner)) return;
-    const int64_t np = div_up(ne, pc);
-    for (int64_t j = (int64_t)((bx + G - (uint32_t)(base % G)) % G); j < np; j += G) {
-      const int64_t s = j * pc;
-      f(off + s, ne - s < pc ? ne - s : pc, bid, k, owner);
-    }
-    base += (uint64_t)np;
-  });
-}
-
 struct DirectShm {
+  uint8_t idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];  // a.idx2rank (walk lookups stay in LDS)
+  char* region[MCCS_DIRECT_MAX_RANKS];                          // me.region
   uint64_t seq;
   uint64_t e_in;                            // E_IN at launch start
   uint64_t e_out[MCCS_DIRECT_MAX_RANKS];    // E_OUT at launch start
@@ -171,7 +196,7 @@ __device__ __forceinline__ void direct_count_out(DirectShm& sh, const mccsDirect
     }
     const uint32_t t = threadIdx.x;
     if (t < a.nranks && t != me.rank && sh.sent[t])
-      __hip_atomic_fetch_add((uint64_t*)(me.region[t] + cnt_base + (int)me.rank * MCCS_FLAG_LINE_BYTES), sh.sent[t],
+      __hip_atomic_fetch_add((uint64_t*)(sh.region[t] + cnt_base + (int)me.rank * MCCS_FLAG_LINE_BYTES), sh.sent[t],
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
@@ -239,22 +264,32 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   const mccsDirectRank& me = a.r[blockIdx.y];
   const int n = (int)a.nranks;
   char* const mine = me.region[me.rank];
-  volatile uint32_t* abortFlag = me.comm ? me.comm->abortFlag : nullptr;
+  volatile uint32_t* abortFlag = me.abort_flag;
   mccsRingKernelCfg ecfg{};
   ecfg.err_line = me.err_line;
   const DirectWalk w = direct_walk<DT>(a);
   const bool one_shot = a.mode == MCCS_DIRECT_ONE_SHOT;
-  if (threadIdx.x == 0) {
-    sh.seq = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_LAUNCHES), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    sh.e_in = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_E_IN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh.ok = !abort_raised(abortFlag);
-    for (int t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t) {
-      sh.e_out[t] = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_E_OUT(t)), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-      sh.owned[t] = 0;
-      sh.sent[t] = 0;
+  MCCS_DTRACE(kDtStart);
+  // Prologue: lanes of wave 0 load the state words (and the abort flag) in
+  // one round trip.
+  if (threadIdx.x < 64) {
+    const uint32_t lane = threadIdx.x;
+    uint64_t v = 0;
+    if (lane < MCCS_DIRECT_ST_WORDS)
+      v = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_STATE) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (lane == MCCS_DIRECT_ST_WORDS)
+      v = abort_raised(abortFlag) ? 1 : 0;
+    if (lane == MCCS_DIRECT_ST_LAUNCHES) sh.seq = v + 1;
+    if (lane == MCCS_DIRECT_ST_E_IN) sh.e_in = v;
+    if (lane >= 2 && lane < MCCS_DIRECT_ST_WORDS) sh.e_out[lane - 2] = v;
+    if (lane == MCCS_DIRECT_ST_WORDS) sh.ok = v == 0;
+    if (lane < MCCS_DIRECT_MAX_RANKS) {
+      sh.owned[lane] = a.owned[lane];
+      sh.sent[lane] = 0;
+      sh.region[lane] = me.region[lane];
     }
-    direct_chunks(w, a, [&](int64_t, int64_t ne, int, int, uint32_t owner) { sh.owned[owner] += (uint64_t)ne; });
+    // the walk's table, 4 bytes per lane
+    ((uint32_t*)sh.idx2rank)[lane] = ((const uint32_t*)a.idx2rank)[lane];
   }
   // Arrival: once every workgroup of the launch has read the start values
   // above, the last to arrive may advance them for the next launch.  The
@@ -267,27 +302,27 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
                                      __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  MCCS_DTRACE(kDtPrologue);
   const uint64_t seq = sh.seq;
   const int64_t esz = (int64_t)sizeof(T);
   const uint32_t G = gridDim.x, bx = blockIdx.x;
   const uint32_t peers = ((1u << n) - 1u) & ~(1u << me.rank);
-  const int64_t piece = a.piece > 0 ? (int64_t)a.piece : 1;
-  const int64_t piece2 = a.piece2 > 0 ? (int64_t)a.piece2 : 1;
-  u32x4 nopre[1];
+  const uint32_t piece = a.piece > 0 ? a.piece : 1;
+  const uint32_t piece2 = a.piece2 > 0 ? a.piece2 : 1;
   __shared__ uint64_t need[MCCS_DIRECT_MAX_RANKS];
   // The last workgroup to arrive advances the running totals and the launch
   // count for the next launch (every workgroup of this one has its copies).
   auto advance = [&]() {
     if (threadIdx.x == 0 && arrived + 1 == G) {
+      uint64_t* st = (uint64_t*)(mine + MCCS_DIRECT_STATE);
       __hip_atomic_store((uint32_t*)(mine + MCCS_DIRECT_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_IN),
-                         sh.e_in + (one_shot ? (uint64_t)w.size : sh.owned[me.rank]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(st + MCCS_DIRECT_ST_E_IN, sh.e_in + (one_shot ? (uint64_t)w.size : sh.owned[me.rank]),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!one_shot)
         for (int t = 0; t < n; ++t)
-          __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_E_OUT(t)), sh.e_out[t] + sh.owned[t], __ATOMIC_RELAXED,
+          __hip_atomic_store(st + MCCS_DIRECT_ST_E_OUT(t), sh.e_out[t] + sh.owned[t], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_LAUNCHES), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(st + MCCS_DIRECT_ST_LAUNCHES, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
 
@@ -296,30 +331,34 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
     const int64_t obase = MCCS_DIRECT_CTRL_BYTES + (int64_t)MCCS_DIRECT_SLOTS * (int64_t)a.slot_bytes +
                           (int64_t)(seq & 1) * MCCS_DIRECT_MAX_RANKS * oslot;
     // 1. broadcast the whole input: pieces of [0, count) to every peer's slot
-    const int64_t np = div_up(w.size, piece);
-    for (int64_t j = bx; j < np && sh.ok; j += G) {
-      const int64_t off = j * piece, ne = w.size - off < piece ? w.size - off : piece;
+    const uint32_t np = (w.size + piece - 1) / piece;
+    for (uint32_t j = bx; j < np && sh.ok; j += G) {
+      const int64_t off = (int64_t)j * piece;
+      const int64_t ne = (int64_t)w.size - off < (int64_t)piece ? (int64_t)w.size - off : (int64_t)piece;
       const void* src[MCCS_DIRECT_MAX_RANKS] = {(const T*)me.send + off};
       void* dst[MCCS_DIRECT_MAX_RANKS];  // slot t: rank t's one-shot slot (none for this rank)
 #pragma unroll
       for (int t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
-        dst[t] = t < n && t != (int)me.rank ? me.region[t] + obase + (int64_t)me.rank * oslot + off * esz : nullptr;
+        dst[t] = t < n && t != (int)me.rank ? sh.region[t] + obase + (int64_t)me.rank * oslot + off * esz : nullptr;
       direct_reduce<DT, OpSum>(src, 1, dst, n, ne);
       if (threadIdx.x == 0)
         for (int t = 0; t < n; ++t) sh.sent[t] += (uint64_t)ne;
     }
+    MCCS_DTRACE(kDtPhase1);
     direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
+    MCCS_DTRACE(kDtCounted1);
     advance();
     // 2. every chunk, reduced in the ring's order into the output
     if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + (uint64_t)w.size;
     __syncthreads();
     bool in_seen = false;  // uniform across the workgroup
-    direct_pieces(w, a, piece2, G, bx, [](uint32_t) { return true; },
+    direct_pieces(w, sh.idx2rank, piece2, G, bx, [](uint32_t) { return true; },
                   [&](int64_t off, int64_t ne, int bid, int k, uint32_t) {
                     if (!sh.ok) return;
                     if (!in_seen) {
                       if (!direct_wait(sh, mine, MCCS_DIRECT_IN_CNT(0), peers, need, abortFlag, a, ecfg)) return;
                       in_seen = true;
+                      MCCS_DTRACE(kDtWait2);
                     }
                     const void* src[MCCS_DIRECT_MAX_RANKS];
                     void* dst[MCCS_DIRECT_MAX_RANKS] = {(T*)me.recv + off};
@@ -329,7 +368,7 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
                       if (j < n) {
                         int idx = k + 1 + j;
                         idx = idx >= n ? idx - n : idx;
-                        const uint32_t q = a.idx2rank[bid][idx];
+                        const uint32_t q = sh.idx2rank[bid][idx];
                         src[j] = q == me.rank ? (const void*)((const T*)me.send + off)
                                               : (const void*)(mine + obase + (int64_t)q * oslot + off * esz);
                       }
@@ -348,25 +387,29 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
     auto own = [&](uint32_t owner) { return owner == me.rank; };
 
     // 1. scatter: every chunk owned by another rank goes to its owner's in slot
-    direct_pieces(w, a, piece, G, bx, others, [&](int64_t off, int64_t ne, int, int, uint32_t owner) {
+    direct_pieces(w, sh.idx2rank, piece, G, bx, others, [&](int64_t off, int64_t ne, int, int, uint32_t owner) {
       if (!sh.ok) return;
-      reduce_copy_rows<DT, OpSum, MCCS_RING_UNROLL, 1, 1, MCCS_RING_INPUT_NT, kPlain>(
-          (const T*)me.send + off, nullptr, in_slot(me.region[owner], me.rank) + off * esz, nullptr, ne, threadIdx.x,
-          blockDim.x, false, nopre);
+      const void* src[MCCS_DIRECT_MAX_RANKS] = {(const T*)me.send + off};
+      void* dst[MCCS_DIRECT_MAX_RANKS] = {in_slot(sh.region[owner], me.rank) + off * esz};
+      direct_reduce<DT, OpSum>(src, 1, dst, 1, ne);
+      MCCS_DTRACE(kDtPiece1);
       if (threadIdx.x == 0) sh.sent[owner] += (uint64_t)ne;
     });
+    MCCS_DTRACE(kDtPhase1);
     direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
+    MCCS_DTRACE(kDtCounted1);
     advance();
 
     // 2. reduce the chunks this rank owns, in the ring's order; broadcast
     if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + sh.owned[me.rank];
     __syncthreads();
     bool in_seen = false;  // uniform across the workgroup, like out_seen below
-    direct_pieces(w, a, piece2, G, bx, own, [&](int64_t off, int64_t ne, int bid, int k, uint32_t) {
+    direct_pieces(w, sh.idx2rank, piece2, G, bx, own, [&](int64_t off, int64_t ne, int bid, int k, uint32_t) {
       if (!sh.ok) return;
       if (!in_seen) {
         if (!direct_wait(sh, mine, MCCS_DIRECT_IN_CNT(0), peers, need, abortFlag, a, ecfg)) return;
         in_seen = true;
+        MCCS_DTRACE(kDtWait2);
       }
       // sources in the ring's order from ring index k+1; destination slot t:
       // rank t's out slot (own: the output)
@@ -379,32 +422,37 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
         if (j < n) {
           int idx = k + 1 + j;
           idx = idx >= n ? idx - n : idx;
-          const uint32_t q = a.idx2rank[bid][idx];
+          const uint32_t q = sh.idx2rank[bid][idx];
           src[j] = q == me.rank ? (const void*)((const T*)me.send + off) : (const void*)(in_slot(mine, q) + off * esz);
-          dst[j] = j == (int)me.rank ? (void*)((T*)me.recv + off) : (void*)(out_slot(me.region[j]) + off * esz);
+          dst[j] = j == (int)me.rank ? (void*)((T*)me.recv + off) : (void*)(out_slot(sh.region[j]) + off * esz);
         }
       }
       direct_reduce<DT, OP>(src, n, dst, n, ne);
       if (threadIdx.x == 0)
         for (int t = 0; t < n; ++t) sh.sent[t] += (uint64_t)ne;
     });
+    MCCS_DTRACE(kDtPhase2);
     direct_count_out(sh, a, me, MCCS_DIRECT_OUT_CNT(0));
+    MCCS_DTRACE(kDtCounted2);
 
     // 3. gather: results of the chunks owned by others, from this rank's out slot
     if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_out[threadIdx.x] + sh.owned[threadIdx.x];
     __syncthreads();
     bool out_seen = false;
-    direct_pieces(w, a, piece, G, bx, others, [&](int64_t off, int64_t ne, int, int, uint32_t) {
+    direct_pieces(w, sh.idx2rank, piece, G, bx, others, [&](int64_t off, int64_t ne, int, int, uint32_t) {
       if (!sh.ok) return;
       if (!out_seen) {
         if (!direct_wait(sh, mine, MCCS_DIRECT_OUT_CNT(0), peers, need, abortFlag, a, ecfg)) return;
         out_seen = true;
+        MCCS_DTRACE(kDtWait3);
       }
-      reduce_copy_rows<DT, OpSum, MCCS_RING_UNROLL, 1, 1, 1, MCCS_RING_OUT_POLICY>(
-          out_slot(mine) + off * esz, nullptr, (T*)me.recv + off, nullptr, ne, threadIdx.x, blockDim.x, false, nopre);
+      const void* src[MCCS_DIRECT_MAX_RANKS] = {out_slot(mine) + off * esz};
+      void* dst[MCCS_DIRECT_MAX_RANKS] = {(T*)me.recv + off};
+      direct_reduce<DT, OpSum>(src, 1, dst, 1, ne);
+      MCCS_DTRACE(kDtPiece3);
     });
   }
-
+  MCCS_DTRACE(kDtEnd);
 }
 
 template <int DT, int OP>

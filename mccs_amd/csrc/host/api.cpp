@@ -34,15 +34,17 @@ static void group_discard() {
 
 // Direct AllReduce thresholds when the config leaves them 0 (MCCS_DIRECT_BYTES /
 // MCCS_ONESHOT_BYTES override): buckets up to this many bytes per rank take
-// the two-shot / one-shot kernel (bit-identical to the ring either way).
-// One-shot to 256 KiB: it beat the ring on the virtual node up to 512 KiB at
-// n = 8 and 2 MiB at n <= 4 (profiles/r03_direct_vnode.json), and over xGMI
-// the ring's 2(n-1) sequential hops only cost more.  Two-shot stays off
-// until the node's sweep (bench config.direct_sweep_fp16) shows where it wins.
-static constexpr int kDirectDefaultBytes = -1;
-static constexpr int kOneshotDefaultBytes = 256 << 10;
+// the one-shot / two-shot kernel (bit-identical to the ring either way).
+// Virtual node, graph replay, fp16 (profiles/r03_direct_vnode.json): one-shot
+// beat the ring at every size to 512 KiB for n = 2 / 4 / 8 and to 2 MiB for
+// n <= 4; two-shot beat it from 32 KiB to 8 MiB at n = 4 and 8 and tied at
+// n = 2 (where the ring is already two hops).  Over xGMI the ring's 2(n-1)
+// sequential hops cost more than here, so these are conservative; the
+// node's sweep (bench config.direct_sweep_fp16) refines them.
+static int default_oneshot_bytes(int nranks) { return nranks <= 4 ? 1 << 20 : 256 << 10; }
+static int default_direct_bytes(int nranks) { return nranks >= 4 ? 4 << 20 : -1; }
 
-static void fill_defaults(mccsCommConfig* c) {
+static void fill_defaults(mccsCommConfig* c, int nranks) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
   if (c->block_threads <= 0) c->block_threads = MCCS_RING_MAX_THREADS;
   if (c->work_fifo_depth <= 0) c->work_fifo_depth = 4096;
@@ -55,8 +57,8 @@ static void fill_defaults(mccsCommConfig* c) {
   // bytes in flight per lane to cover an xGMI hop; 2 x the FIFO memory
   // (8 MiB per connection)
   if (c->fifo_slots == 0) c->fifo_slots = 2 * MCCS_BUFFER_SLOTS;
-  if (c->direct_bytes == 0) c->direct_bytes = kDirectDefaultBytes;
-  if (c->oneshot_bytes == 0) c->oneshot_bytes = kOneshotDefaultBytes;
+  if (c->direct_bytes == 0) c->direct_bytes = default_direct_bytes(nranks);
+  if (c->oneshot_bytes == 0) c->oneshot_bytes = default_oneshot_bytes(nranks);
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
@@ -85,7 +87,7 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   mccsCommConfig cfg;
   mccsCommConfigDefault(&cfg);
   if (user_cfg) cfg = *user_cfg;
-  fill_defaults(&cfg);
+  fill_defaults(&cfg, nranks);
   MCCS_CHECK(validate_cfg(cfg, nranks));
   if (rank < 0 || rank >= nranks) return mccsInvalidArgument;
   int ndev = 0;

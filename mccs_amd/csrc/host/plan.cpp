@@ -450,6 +450,21 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
     const int pos0 = (int)(std::find(ring.begin(), ring.end(), 0) - ring.begin());
     for (int k = 0; k < n; ++k) da->idx2rank[bid][k] = (uint8_t)ring[(pos0 + k) % n];
   }
+  // elements each rank owns: the ring walk (all_reduce.h:28-42), chunk k of
+  // channel bid owned by the rank at ring index k
+  {
+    const int64_t size = (int64_t)da->count, parts = (int64_t)da->nch * n;
+    const int64_t chunk = (int64_t)((int)da->buff_size / MCCS_BUFFER_SLOTS / (int)esize) * ALLREDUCE_CHUNKSTEPS;
+    const int64_t gran = std::max<int64_t>(1, (int64_t)(nthr - WARP_SIZE) * 8 / (int64_t)esize);
+    for (int64_t g = 0; g < size; g += parts * chunk) {
+      int64_t rcs = std::min(chunk, (size - g + parts - 1) / parts);
+      rcs = (rcs + gran - 1) / gran * gran;
+      for (int64_t c = 0; c < parts; ++c) {
+        const int64_t off = g + c * rcs;
+        if (off < size) da->owned[da->idx2rank[c / n][c % n]] += (uint64_t)std::min(rcs, size - off);
+      }
+    }
+  }
   for (size_t k = 0; k < idx.size(); ++k) {
     const Comm* ck = comms[idx[k]];
     mccsDirectRank& r = da->r[k];
@@ -460,6 +475,7 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
       r.region[t] = ck->peer_arena[t] + ck->layout.direct_off();
     }
     r.comm = (mccsDevComm*)ck->d_comm;
+    r.abort_flag = ck->d_abort;
     r.rank = (uint32_t)ck->rank;
     r.err_line = 1;
     // safest hand-off of the group, as for the ring (SYSTEM > UNCACHED_RELEASE > UNCACHED)

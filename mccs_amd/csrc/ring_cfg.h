@@ -138,10 +138,15 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 #define MCCS_DIRECT_CTRL_BYTES 65536
 #define MCCS_DIRECT_IN_CNT(s) ((s) * MCCS_FLAG_LINE_BYTES)             // u64, added to by sender s
 #define MCCS_DIRECT_OUT_CNT(o) (1024 + (o) * MCCS_FLAG_LINE_BYTES)     // u64, added to by owner o
-#define MCCS_DIRECT_E_IN 2048                                          // u64: elements each sender sent so far
-#define MCCS_DIRECT_E_OUT(o) (2048 + 64 + (o) * 8)                     // u64: elements owner o broadcast so far
+// u64 state words (one line, read by one wave load): launches completed,
+// E_IN (elements each sender has sent so far), E_OUT[o] (elements owner o
+// has broadcast so far)
+#define MCCS_DIRECT_STATE 2048
+#define MCCS_DIRECT_ST_LAUNCHES 0
+#define MCCS_DIRECT_ST_E_IN 1
+#define MCCS_DIRECT_ST_E_OUT(o) (2 + (o))
+#define MCCS_DIRECT_ST_WORDS (2 + MCCS_DIRECT_MAX_RANKS)
 #define MCCS_DIRECT_DONE 4096                                          // u32: workgroups arrived in the launch
-#define MCCS_DIRECT_LAUNCHES 4224                                      // u64: launches completed
 #define MCCS_DIRECT_SLOTS (MCCS_DIRECT_MAX_RANKS + 1)                  // two-shot slots
 #define MCCS_DIRECT_THREADS 512
 #define MCCS_DIRECT_TWO_SHOT 0
@@ -151,7 +156,8 @@ struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
   const void* send;
   void* recv;
   char* region[MCCS_DIRECT_MAX_RANKS];  // every rank's direct region as this rank maps it
-  struct mccsDevComm* comm;             // abortFlag
+  struct mccsDevComm* comm;             // the rank's device communicator
+  uint32_t* abort_flag;                 // comm->abortFlag (one load less in the prologue)
   uint32_t rank;
   uint32_t err_line;
 };
@@ -166,6 +172,7 @@ struct mccsDirectArgs {
   uint32_t mode;                              // MCCS_DIRECT_TWO_SHOT / ONE_SHOT
   uint32_t piece;                             // elements per piece of the scatter / gather phases
   uint32_t piece2;                            // elements per piece of the reduction phase
+  uint64_t owned[MCCS_DIRECT_MAX_RANKS];      // elements of the walk's chunks each rank owns
   uint8_t idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];  // rank at ring index k of channel bid
 };
 #ifdef __cplusplus

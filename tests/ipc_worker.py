@@ -47,7 +47,12 @@ def main():
                  "sender-uncached": (C.FIFO_UNCACHED, C.LOCALITY_SENDER),
                  "sender-device": (C.FIFO_DEVICE, C.LOCALITY_SENDER),
                  "release": (C.FIFO_UNCACHED_RELEASE, C.LOCALITY_RECEIVER),
-                 "sender-release": (C.FIFO_UNCACHED_RELEASE, C.LOCALITY_SENDER)}
+                 "sender-release": (C.FIFO_UNCACHED_RELEASE, C.LOCALITY_SENDER),
+                 # the direct kernel (two-shot / one-shot) over IPC-mapped arenas
+                 "direct": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
+                 "oneshot": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
+    direct_kw = {"direct": dict(direct_bytes=8 << 20, oneshot_bytes=-1),
+                 "oneshot": dict(direct_bytes=-1, oneshot_bytes=8 << 20)}
     names = os.environ.get("IPC_MODES", "uncached,device").split(",")
     results = {}
     # processes sharing one GPU: the library's default lanes; mccsCommConnect
@@ -57,7 +62,8 @@ def main():
     for mode in names:
         fifo, loc = all_modes[mode]
         comm = C.init_communicator_rank(rank, world, dev, exchange,
-                                        C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, lanes=lanes))
+                                        C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, lanes=lanes,
+                                                     **direct_kw.get(mode, {})))
         cases = [(2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)]
         nfuzz = int(os.environ.get("IPC_FUZZ", "0"))
         if nfuzz:  # seeded random dtypes / ragged counts, same on every rank
@@ -85,7 +91,30 @@ def main():
             except Exception as e:  # noqa: BLE001
                 print(f"[rank {rank}] {mode} code={code}: {e}", flush=True)
                 ok = False
+            if mode in direct_kw:  # the call really took that kernel
+                ok = ok and comm.last_algo() == mode
             results[f"{mode}/dtype{code}/n{count}"] = ok
+        if mode in direct_kw:  # several launches back to back, fresh inputs each, then one sync
+            k = 12
+            rng = np.random.default_rng(99 + rank)
+            xs_all, sends, recvs = [], [], []
+            for i in range(k):
+                x = vnode.gen(7, 100003 + i, rng)
+                xa = [None] * world
+                dist.all_gather_object(xa, x)
+                xs_all.append(xa)
+                sends.append(vnode.to_dev(x))
+                recvs.append(vnode.to_dev(np.zeros_like(x)))
+            for i in range(k):
+                C.all_reduce(comm, sends[i], recvs[i], 100003 + i, 7, 0)
+            comm.sync()
+            ok = True
+            for i in range(k):
+                p = vnode.Planner(comm.nchannels, comm.rings())
+                nch, nthr, rings = p.select((100003 + i) * 4, 0)
+                exp = orc.ring_allreduce(7, 0, xs_all[i], nchannels=nch, nthreads=nthr, ring_orders=rings)
+                ok = ok and bool(np.array_equal(vnode.from_dev(recvs[i], 7).view(np.uint8), exp.view(np.uint8)))
+            results[f"{mode}/back_to_back_x{k}"] = ok
         if torch.cuda.device_count() < world:  # co-located processes: lanes shrunk to half the ring slots
             # auto lanes (api.cpp make_comm) capped at half of MI355X's 256 one-per-CU ring slots
             auto = (128 if world == 2 else 64) // comm.nchannels

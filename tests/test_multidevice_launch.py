@@ -20,7 +20,6 @@ from mccs_amd import _lib
 from mccs_amd import comm as C
 
 F32, SUM = 7, 0
-DIRECT_DEFAULTS = True  # conftest: these tests set the direct thresholds themselves
 
 
 def _parse(line):
@@ -330,9 +329,9 @@ def test_direct_allreduce_plans(fake):
 
 
 def test_direct_defaults_and_fused_ranks(fake, monkeypatch):
-    """Library defaults: one-shot up to 256 KiB, the ring above (two-shot
-    off); fused ranks on one device share one direct launch; without peer
-    atomics every AllReduce takes the ring."""
+    """Library defaults at n = 2: one-shot up to 1 MiB, the ring above
+    (two-shot off below 4 ranks); fused ranks on one device share one direct
+    launch; without peer atomics every AllReduce takes the ring."""
     for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES"):
         monkeypatch.delenv(k, raising=False)
     fake(2)
@@ -348,7 +347,7 @@ def test_direct_defaults_and_fused_ranks(fake, monkeypatch):
             c.sync()
         plain = C.init_all([0, 1])
         assert all(c.direct_enabled() for c in plain)
-        for count, want in ((1000, "oneshot"), (65536, "oneshot"), (65537, "ring")):
+        for count, want in ((1000, "oneshot"), (262144, "oneshot"), (262145, "ring")):
             _log()
             _allreduce_group(plain, count=count)
             assert [kv["kind"] for k, kv in _log() if k == "launch"] == (["direct"] * 2 if want != "ring" else
@@ -389,6 +388,26 @@ def test_oneshot_below_its_threshold(fake):
                     assert kv["kind"] == "direct" and kv["mode"] == mode
                     for p in (int(kv["piece"]), int(kv["piece2"])):
                         assert 1024 <= p <= 16384  # fp32 elements: 4..64 KiB
+        for c in comms:
+            c.sync()
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+@pytest.mark.parametrize("n,oneshot,direct", [(4, 1 << 20, 4 << 20), (8, 256 << 10, 4 << 20), (3, 1 << 20, None)])
+def test_direct_default_thresholds(fake, monkeypatch, n, oneshot, direct):
+    for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES"):
+        monkeypatch.delenv(k, raising=False)
+    fake(n)
+    comms = C.init_all(list(range(n)))
+    try:
+        cases = [(oneshot // 4, "oneshot"), (oneshot // 4 + 1, "direct" if direct else "ring")]
+        if direct:
+            cases += [(direct // 4, "direct"), (direct // 4 + 1, "ring")]
+        for count, want in cases:
+            _allreduce_group(comms, count=count)
+            assert [c.last_algo() for c in comms] == [want] * n, (count, want)
         for c in comms:
             c.sync()
     finally:
