@@ -374,6 +374,9 @@ def size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20, graph_upt
     return rows
 
 
+from ._streams import side_stream  # noqa: E402
+
+
 def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, ring_rows, upto=8 << 20,
                  oneshot_upto=2 << 20, warmup=3, K=20):
     """The direct AllReduce variants (direct_kernel.h) beside the ring over the
@@ -381,57 +384,99 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
     the measured transport's config, every size exact-sum validated, eager
     and graph-replayed latency per call (max over ranks).  ring_rows: the
     size sweep's rows of the ring.  Ends with the thresholds the table
-    supports (the largest size each variant still beats the ring)."""
+    supports (the largest size each variant still beats the ring).
+
+    Informational and failure-isolated: each measurement runs with no
+    collective inside it, the ranks then agree on its success, and a variant
+    that fails anywhere (no peer atomics, watchdog, wrong sum) is recorded
+    and dropped on every rank without failing the line."""
     import dataclasses
 
     out = {"sizes": [nb for nb in SWEEP_BYTES if nb <= upto], "rows": []}
     ring = {r["bytes"]: r for r in ring_rows}
-    comms = {}
-    try:
-        for algo, kw in (("direct", dict(direct_bytes=upto, oneshot_bytes=-1)),
-                         ("oneshot", dict(direct_bytes=-1, oneshot_bytes=oneshot_upto))):
-            cfg = dataclasses.replace(config or C.CommConfig(), **kw)
+    comms, dead = {}, {}
+    code = C.AllReduceDataType.Float16
+    for algo, kw in (("direct", dict(direct_bytes=upto, oneshot_bytes=-1)),
+                     ("oneshot", dict(direct_bytes=-1, oneshot_bytes=oneshot_upto))):
+        cfg = dataclasses.replace(config or C.CommConfig(), **kw)
+        try:
             comms[algo] = C.init_communicator_rank(rank, world, device, exchange, cfg)
-        for nb in out["sizes"]:
-            n = nb // 2
-            x = torch.empty(n, dtype=torch.float16, device=dev).uniform_(-1, 1)
-            y = torch.empty_like(x)
-            row = {"bytes": nb}
-            if nb in ring:
-                row["ring_us"] = ring[nb]["latency_us"]
-                if "graph_latency_us" in ring[nb]:
-                    row["ring_graph_us"] = ring[nb]["graph_latency_us"]
-            for algo, cm in comms.items():
-                if algo == "oneshot" and nb > oneshot_upto:
-                    continue
-
-                def step(cm=cm):
-                    C.all_reduce(cm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum)
-
-                el = max_over_ranks(dist, time_steps(torch, dist, cm, step, warmup, K)) / K
-                require(dist, cm.last_algo() == algo, f"{algo} sweep {nb} B took {cm.last_algo()}")
-                gl = graph_replay(torch, dist, cm, lambda st, cm=cm: C.all_reduce(
-                    cm, x, y, n, C.AllReduceDataType.Float16, C.AllReduceOpType.Sum, st), calls=10)
-                require(dist, exact_sum_ok(torch, C, cm, rank, world, n, torch.float16,
-                                           C.AllReduceDataType.Float16, dev), f"{algo} sweep {nb} B")
-                row[f"{algo}_us"] = round(el * 1e6, 2)
-                row[f"{algo}_graph_us"] = round(gl * 1e6, 2)
-            out["rows"].append(row)
-            del x, y
-        best = {}
-        for algo in ("direct", "oneshot"):
-            wins = [r["bytes"] for r in out["rows"] if f"{algo}_graph_us" in r and "ring_graph_us" in r
-                    and r[f"{algo}_graph_us"] < r["ring_graph_us"]]
-            best[f"{algo}_beats_ring_upto_bytes"] = max(wins) if wins else 0
-        out["summary"] = best
-    except BenchFailure:
-        raise
-    except Exception as e:  # noqa: BLE001  (informational leg: recorded, never fatal)
-        out["error"] = f"{type(e).__name__}: {e}"[:300]
-    finally:
+            ok = comms[algo].direct_enabled()
+            err = None if ok else "direct kernel disabled: no peer atomics between these devices"
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, f"{type(e).__name__}: {e}"[:200]
+        if not agree(dist, ok):
+            dead[algo] = err or "failed on another rank"
+    out["p2p_atomics"] = "direct" not in dead or "peer atomics" not in dead.get("direct", "")
+    for nb in out["sizes"]:
+        n = nb // 2
+        x = torch.empty(n, dtype=torch.float16, device=dev).uniform_(-1, 1)
+        y = torch.empty_like(x)
+        row = {"bytes": nb}
+        if nb in ring:
+            row["ring_us"] = ring[nb]["latency_us"]
+            if "graph_latency_us" in ring[nb]:
+                row["ring_graph_us"] = ring[nb]["graph_latency_us"]
+        for algo, cm in comms.items():
+            if algo in dead or (algo == "oneshot" and nb > oneshot_upto):
+                continue
+            el = gl = None
+            err = None
+            dist.barrier()
+            try:
+                for _ in range(warmup):
+                    C.all_reduce(cm, x, y, n, code, C.AllReduceOpType.Sum)
+                torch.cuda.synchronize()
+                cm.sync()
+                t0 = time.perf_counter()
+                for _ in range(K):
+                    C.all_reduce(cm, x, y, n, code, C.AllReduceOpType.Sum)
+                torch.cuda.synchronize()
+                cm.sync()
+                el = (time.perf_counter() - t0) / K
+                if cm.last_algo() != algo:
+                    raise RuntimeError(f"took {cm.last_algo()}")
+                gs = side_stream(torch, slot=1)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=gs):
+                    for _ in range(10):
+                        C.all_reduce(cm, x, y, n, code, C.AllReduceOpType.Sum, gs)
+                g.replay()
+                torch.cuda.synchronize()
+                cm.sync()
+                t0 = time.perf_counter()
+                g.replay()
+                torch.cuda.synchronize()
+                cm.sync()
+                gl = (time.perf_counter() - t0) / 10
+                del g
+                if not exact_sum_ok(torch, C, cm, rank, world, n, torch.float16, code, dev):
+                    raise RuntimeError("exact-sum check failed")
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"[:200]
+            if not agree(dist, err is None):
+                dead[algo] = f"{nb} B: " + (err or "failed on another rank")
+                continue
+            row[f"{algo}_us"] = round(max_over_ranks(dist, el) * 1e6, 2)
+            row[f"{algo}_graph_us"] = round(max_over_ranks(dist, gl) * 1e6, 2)
+        out["rows"].append(row)
+        del x, y
+    best = {}
+    for algo in ("direct", "oneshot"):
+        wins = [r["bytes"] for r in out["rows"] if f"{algo}_graph_us" in r and "ring_graph_us" in r
+                and r[f"{algo}_graph_us"] < r["ring_graph_us"]]
+        best[f"{algo}_beats_ring_upto_bytes"] = max(wins) if wins else 0
+    out["summary"] = best
+    if dead:
+        out["failed"] = dead
+    try:
         torch.cuda.synchronize()
+    finally:
         for cm in comms.values():
-            cm.destroy()
+            try:
+                cm.destroy()
+            except Exception:  # noqa: BLE001
+                pass
         dist.barrier()
     return out
 
