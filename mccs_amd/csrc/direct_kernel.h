@@ -37,6 +37,10 @@
 //        of this launch's parity; drain; add to every peer's IN_CNT line;
 //     2. reduce: wait for every peer's input; every chunk, in the ring's
 //        order, straight into the output.
+//   AllGather one-shot (all_gather.h's result, byte for byte)
+//     1. this rank's segment -> every peer's one-shot slot and its own place
+//        in the output; drain; count out;
+//     2. wait; every peer's segment from its slot to its place.
 // The hand-off policy follows the ring's (mccsRingKernelCfg fence modes):
 // drains only for uncached arenas, a system-scope release before the count
 // and an acquire after a wait otherwise (each workgroup fences its own
@@ -268,7 +272,8 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   mccsRingKernelCfg ecfg{};
   ecfg.err_line = me.err_line;
   const DirectWalk w = direct_walk<DT>(a);
-  const bool one_shot = a.mode == MCCS_DIRECT_ONE_SHOT;
+  const bool ag = a.mode == MCCS_DIRECT_AG_ONE_SHOT;  // AllGather: bytes, no reduction
+  const bool one_shot = a.mode == MCCS_DIRECT_ONE_SHOT || ag;
   MCCS_DTRACE(kDtStart);
   // Prologue: lanes of wave 0 load the state words (and the abort flag) in
   // one round trip.
@@ -336,10 +341,15 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
       const int64_t off = (int64_t)j * piece;
       const int64_t ne = (int64_t)w.size - off < (int64_t)piece ? (int64_t)w.size - off : (int64_t)piece;
       const void* src[MCCS_DIRECT_MAX_RANKS] = {(const T*)me.send + off};
-      void* dst[MCCS_DIRECT_MAX_RANKS];  // slot t: rank t's one-shot slot (none for this rank)
+      // slot t: rank t's one-shot slot; this rank: nothing, or (AllGather)
+      // its own segment of the output
+      void* dst[MCCS_DIRECT_MAX_RANKS];
 #pragma unroll
       for (int t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
-        dst[t] = t < n && t != (int)me.rank ? sh.region[t] + obase + (int64_t)me.rank * oslot + off * esz : nullptr;
+        dst[t] = t >= n                 ? nullptr
+                 : t != (int)me.rank    ? (void*)(sh.region[t] + obase + (int64_t)me.rank * oslot + off * esz)
+                 : ag                   ? (void*)((T*)me.recv + (int64_t)me.rank * w.size + off)
+                                        : nullptr;
       direct_reduce<DT, OpSum>(src, 1, dst, n, ne);
       if (threadIdx.x == 0)
         for (int t = 0; t < n; ++t) sh.sent[t] += (uint64_t)ne;
@@ -348,10 +358,33 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
     direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
     MCCS_DTRACE(kDtCounted1);
     advance();
-    // 2. every chunk, reduced in the ring's order into the output
     if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + (uint64_t)w.size;
     __syncthreads();
     bool in_seen = false;  // uniform across the workgroup
+    if (ag) {
+      // 2. (AllGather) every peer's segment, from its slot to the output;
+      // pieces of the n-1 segments dealt round-robin
+      uint32_t base = 0;
+      const uint32_t nps = (w.size + piece2 - 1) / piece2;
+      for (uint32_t t = 0; t < (uint32_t)n; ++t) {
+        if (t == me.rank) continue;
+        for (uint32_t j = bx >= base ? bx - base : bx + G - base; j < nps && sh.ok; j += G) {
+          if (!in_seen) {
+            if (!direct_wait(sh, mine, MCCS_DIRECT_IN_CNT(0), peers, need, abortFlag, a, ecfg)) break;
+            in_seen = true;
+            MCCS_DTRACE(kDtWait2);
+          }
+          const int64_t off = (int64_t)j * piece2;
+          const int64_t ne = (int64_t)w.size - off < (int64_t)piece2 ? (int64_t)w.size - off : (int64_t)piece2;
+          const void* src[MCCS_DIRECT_MAX_RANKS] = {mine + obase + (int64_t)t * oslot + off * esz};
+          void* dst[MCCS_DIRECT_MAX_RANKS] = {(T*)me.recv + (int64_t)t * w.size + off};
+          direct_reduce<DT, OpSum>(src, 1, dst, 1, ne);
+        }
+        base += nps;
+        while (base >= G) base -= G;
+      }
+    } else
+    // 2. every chunk, reduced in the ring's order into the output
     direct_pieces(w, sh.idx2rank, piece2, G, bx, [](uint32_t) { return true; },
                   [&](int64_t off, int64_t ne, int bid, int k, uint32_t) {
                     if (!sh.ok) return;

@@ -117,10 +117,13 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   // One AllReduce that fits the direct region (every rank decides alike: same
   // call, same config) is held for the direct kernel; the launch may still
   // send it to the ring (plan_launch_group).
-  const size_t bytes = count * (size_t)elem_bytes(dtype);
+  // (AllGather: count is bytes per rank; its one-shot moves the ring's link
+  // bytes in one exchange instead of n-1 hops)
+  const size_t bytes = func == mccsFuncAllGather ? count : count * (size_t)elem_bytes(dtype);
   const bool oneshot = c->layout.oneshot_slot > 0 && bytes <= (size_t)c->cfg.oneshot_bytes;
-  const bool twoshot = c->layout.direct_slot > 0 && bytes <= (size_t)c->cfg.direct_bytes;
-  if (!c->plan_pending && func == mccsFuncAllReduce && c->direct_ok && (oneshot || twoshot)) {
+  const bool twoshot = func == mccsFuncAllReduce && c->layout.direct_slot > 0 && bytes <= (size_t)c->cfg.direct_bytes;
+  if (!c->plan_pending && (func == mccsFuncAllReduce || func == mccsFuncAllGather) && c->direct_ok &&
+      (oneshot || twoshot)) {
     c->plan_direct = true;
     c->direct.send = send;
     c->direct.recv = recv;
@@ -410,7 +413,8 @@ static bool direct_group(std::vector<Comm*>& comms, const std::vector<int>& idx)
   for (size_t k = 0; k < idx.size(); ++k) {
     const Comm* ck = comms[idx[k]];
     if (!ck->plan_direct) return false;
-    if (ck->nranks != c0->nranks || ck->direct.count != c0->direct.count || ck->plan_dtype != c0->plan_dtype ||
+    if (ck->nranks != c0->nranks || ck->direct.count != c0->direct.count || ck->plan_func != c0->plan_func ||
+        ck->plan_dtype != c0->plan_dtype ||
         ck->plan_op != c0->plan_op || ck->rings != c0->rings || ck->cfg.buffer_size != c0->cfg.buffer_size ||
         ck->layout.direct_slot != c0->layout.direct_slot || ck->layout.oneshot_slot != c0->layout.oneshot_slot ||
         ck->cfg.oneshot_bytes != c0->cfg.oneshot_bytes || ck->cfg.direct_bytes != c0->cfg.direct_bytes ||
@@ -427,7 +431,8 @@ static bool direct_group(std::vector<Comm*>& comms, const std::vector<int>& idx)
 static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<int>& idx, mccsDirectArgs* da,
                                  unsigned* grid_x) {
   const Comm* c0 = comms[idx[0]];
-  const size_t esize = (size_t)elem_bytes(c0->plan_dtype);
+  const bool gather = c0->plan_func == mccsFuncAllGather;
+  const size_t esize = gather ? 1 : (size_t)elem_bytes(c0->plan_dtype);
   int nch = 0, nthr = 0;
   task_schema(c0->direct.count * esize, c0->nch, &nch, &nthr);
   const std::vector<int> chans = select_channels(c0, nch);
@@ -438,7 +443,7 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   da->oslot_bytes = c0->layout.oneshot_slot;
   const size_t nbytes = (size_t)c0->direct.count * esize;
   const bool oneshot = c0->layout.oneshot_slot > 0 && nbytes <= (size_t)c0->cfg.oneshot_bytes;
-  da->mode = oneshot ? MCCS_DIRECT_ONE_SHOT : MCCS_DIRECT_TWO_SHOT;
+  da->mode = gather ? MCCS_DIRECT_AG_ONE_SHOT : oneshot ? MCCS_DIRECT_ONE_SHOT : MCCS_DIRECT_TWO_SHOT;
   da->nranks = (uint32_t)n;
   da->nch = (uint32_t)chans.size();
   da->nthr_ref = (uint32_t)nthr;
@@ -451,8 +456,8 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
     for (int k = 0; k < n; ++k) da->idx2rank[bid][k] = (uint8_t)ring[(pos0 + k) % n];
   }
   // elements each rank owns: the ring walk (all_reduce.h:28-42), chunk k of
-  // channel bid owned by the rank at ring index k
-  {
+  // channel bid owned by the rank at ring index k (AllGather: unused)
+  if (!gather) {
     const int64_t size = (int64_t)da->count, parts = (int64_t)da->nch * n;
     const int64_t chunk = (int64_t)((int)da->buff_size / MCCS_BUFFER_SLOTS / (int)esize) * ALLREDUCE_CHUNKSTEPS;
     const int64_t gran = std::max<int64_t>(1, (int64_t)(nthr - WARP_SIZE) * 8 / (int64_t)esize);
@@ -491,7 +496,8 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   // 4 KiB steps (aligned: chunk offsets are granule multiples), 4..64 KiB.
   // One-shot: phase 1 sends the whole input, phase 2 reduces all of it.
   const size_t bytes = nbytes;
-  const size_t scatter = oneshot ? bytes : bytes - bytes / n;  // two-shot phases 1 and 3: chunks others own
+  // two-shot phases 1 and 3: the chunks others own; AllGather phase 2: n-1 segments
+  const size_t scatter = gather ? bytes * (n - 1) : oneshot ? bytes : bytes - bytes / n;
   const int cap = coresident_direct_blocks(c0->device);
   long g = std::min<long>((long)((scatter + 8191) / 8192), direct_max_blocks());
   if (idx.size() > 1) g = std::min<long>(g, cap / (long)idx.size());  // one fused launch: co-scheduled
@@ -508,8 +514,8 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
     p = std::min<size_t>(std::max<size_t>((p + 4095) & ~(size_t)4095, 4096), 65536);
     return (uint32_t)(p / esize);
   };
-  da->piece = piece(scatter);
-  da->piece2 = piece(oneshot ? bytes : bytes / n + 1);
+  da->piece = piece(gather ? bytes : scatter);
+  da->piece2 = piece(gather ? scatter : oneshot ? bytes : bytes / n + 1);
   for (size_t k = 0; k < idx.size(); ++k) {
     Comm* ck = comms[idx[k]];
     ck->plan_direct = false;
@@ -561,7 +567,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     Comm* c0 = comms[idx[0]];
     if (direct) {
       MCCS_CHECK(build_direct(comms, idx, &da, &grid));
-      fn = direct_kernel_ptr(c0->plan_dtype, c0->plan_op);
+      fn = c0->plan_func == mccsFuncAllGather ? direct_kernel_ptr(mccsInt8, mccsDevSum)
+                                              : direct_kernel_ptr(c0->plan_dtype, c0->plan_op);
       if (!fn) return mccsInvalidArgument;
       block = MCCS_DIRECT_THREADS;
       args[0] = &da;
@@ -645,8 +652,9 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
     for (size_t k = 0; k < idx.size(); ++k) {
       comms[idx[k]]->event_recorded = record;
-      comms[idx[k]]->last_algo = !direct ? MCCS_ALGO_RING : da.mode == MCCS_DIRECT_ONE_SHOT ? MCCS_ALGO_ONESHOT
-                                                                                         : MCCS_ALGO_DIRECT;
+      comms[idx[k]]->last_algo = !direct                            ? MCCS_ALGO_RING
+                                 : da.mode == MCCS_DIRECT_TWO_SHOT ? MCCS_ALGO_DIRECT
+                                                                   : MCCS_ALGO_ONESHOT;
     }
     c0->event_recorded = record || stop_on_launch;
   }

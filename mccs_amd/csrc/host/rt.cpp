@@ -238,7 +238,9 @@ class FakeRuntime final : public DeviceRuntime {
         for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(da->r[k].comm) == cur_;
         extra = " count=" + std::to_string(da->count) + " nch=" + std::to_string(da->nch) +
                 " nthr=" + std::to_string(da->nthr_ref) + " fence=" + std::to_string(da->fence_mode) +
-                " mode=" + (da->mode == MCCS_DIRECT_ONE_SHOT ? "oneshot" : "twoshot") +
+                " mode=" + (da->mode == MCCS_DIRECT_ONE_SHOT      ? "oneshot"
+                            : da->mode == MCCS_DIRECT_AG_ONE_SHOT ? "ag-oneshot"
+                                                                  : "twoshot") +
                 " piece=" + std::to_string(da->piece) + " piece2=" + std::to_string(da->piece2);
       } else {
         const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];

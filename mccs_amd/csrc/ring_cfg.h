@@ -151,6 +151,7 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 #define MCCS_DIRECT_THREADS 512
 #define MCCS_DIRECT_TWO_SHOT 0
 #define MCCS_DIRECT_ONE_SHOT 1
+#define MCCS_DIRECT_AG_ONE_SHOT 2  // AllGather: count = bytes per rank (dtype int8)
 
 struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
   const void* send;
@@ -169,7 +170,7 @@ struct mccsDirectArgs {
   uint64_t timeout_ticks;  // s_memrealtime ticks; 0 = never
   uint32_t nranks, nch, nthr_ref, buff_size;  // the ring walk this launch reproduces
   uint32_t fence_mode;                        // MCCS_FENCE_*
-  uint32_t mode;                              // MCCS_DIRECT_TWO_SHOT / ONE_SHOT
+  uint32_t mode;                              // MCCS_DIRECT_TWO_SHOT / ONE_SHOT / AG_ONE_SHOT
   uint32_t piece;                             // elements per piece of the scatter / gather phases
   uint32_t piece2;                            // elements per piece of the reduction phase
   uint64_t owned[MCCS_DIRECT_MAX_RANKS];      // elements of the walk's chunks each rank owns

@@ -326,3 +326,133 @@ def test_library_defaults(orc):
             _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
+
+
+def _allgather(comms, bufs_in, nbytes, inplace):
+    """One grouped AllGather; returns each rank's output as bytes."""
+    import torch
+
+    n = len(comms)
+    outs = []
+    with C.group():
+        for r in range(n):
+            if inplace:  # allgather_proto: send = own segment of the output buffer
+                out = torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda")
+                out[r * nbytes:(r + 1) * nbytes].copy_(bufs_in[r])
+                C.all_gather(comms[r], out[r * nbytes:], out, nbytes)
+            else:
+                out = torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda")
+                C.all_gather(comms[r], bufs_in[r], out, nbytes)
+            outs.append(out)
+    for c in comms:
+        c.sync()
+    return [o.cpu().numpy() for o in outs]
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("nbytes", [1, 1000, 4096, 65539, 1 << 20])
+def test_allgather_oneshot(n, nbytes, inplace):
+    """AllGather buckets up to oneshot_bytes take the one-shot exchange: every
+    rank's segment lands in every output byte for byte (all_gather.h's
+    result), in place (allgather_proto's layout) or not."""
+    import torch
+
+    comms = C.init_all([0] * n, _cfg("oneshot"))
+    try:
+        rng = np.random.default_rng(nbytes + n)
+        data = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(n)]
+        bufs = [torch.from_numpy(d).cuda() for d in data]
+        outs = _allgather(comms, bufs, nbytes, inplace)
+        _algo(comms, "oneshot")
+        exp = np.concatenate(data)
+        for r, o in enumerate(outs):
+            assert np.array_equal(o, exp), f"rank {r}"
+    finally:
+        vnode.destroy(comms)
+
+
+def test_allgather_oneshot_back_to_back_and_mixed(orc):
+    """AllGathers (one-shot and, above the threshold, ring) and AllReduces
+    (one-shot, two-shot) alternate without syncs in between; every output
+    exact (the one-shot slots' parity and the running counts are shared by
+    both collectives)."""
+    import torch
+
+    n = 4
+    comms = C.init_all([0] * n, C.CommConfig(direct_bytes=1 << 20, oneshot_bytes=64 << 10))
+    try:
+        rng = np.random.default_rng(77)
+        plan = [("ag", 5000), ("ar", 3000), ("ag", 70000), ("ar", 100000), ("ag", 65536), ("ar", 7), ("ag", 1)] * 3
+        keep = []
+        for kind, size in plan:
+            if kind == "ag":
+                data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(n)]
+                src = [torch.from_numpy(d).cuda() for d in data]
+                out = [torch.zeros(n * size, dtype=torch.uint8, device="cuda") for _ in range(n)]
+                with C.group():
+                    for r in range(n):
+                        C.all_gather(comms[r], src[r], out[r], size)
+                keep.append((kind, size, data, src, out, [c.last_algo() for c in comms]))
+            else:
+                data = [vnode.gen(F32, size, rng) for _ in range(n)]
+                src = [vnode.to_dev(x) for x in data]
+                out = [vnode.to_dev(np.zeros_like(x)) for x in data]
+                with C.group():
+                    for r in range(n):
+                        C.all_reduce(comms[r], src[r], out[r], size, F32, 0)
+                keep.append((kind, size, data, src, out, [c.last_algo() for c in comms]))
+        torch.cuda.synchronize()
+        for c in comms:
+            c.sync()
+        for kind, size, data, src, out, algos in keep:
+            if kind == "ag":
+                assert algos == ["oneshot" if size <= 64 << 10 else "ring"] * n, (size, algos)
+                exp = np.concatenate(data)
+                for r in range(n):
+                    assert np.array_equal(out[r].cpu().numpy(), exp), (size, r)
+            else:
+                nb = size * 4
+                assert algos == ["oneshot" if nb <= 64 << 10 else "direct"] * n, (size, algos)
+                exp = vnode.expected_allreduce(orc, data, F32, 0, comms[0])
+                _check([vnode.from_dev(out[r], F32) for r in range(n)], exp)
+    finally:
+        vnode.destroy(comms)
+
+
+def test_allgather_oneshot_captured_in_hip_graph():
+    import torch
+
+    n, size = 3, 40000
+    comms = C.init_all([0] * n, _cfg("oneshot"))
+    try:
+        rng = np.random.default_rng(5)
+        src = [torch.zeros(size, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        out = [torch.zeros(n * size, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        s = torch.cuda.Stream()
+        with C.group():
+            for r in range(n):
+                C.all_gather(comms[r], src[r], out[r], size, stream=s)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(2):
+                with C.group():
+                    for r in range(n):
+                        C.all_gather(comms[r], src[r], out[r], size, stream=s)
+        for it in range(3):
+            data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(n)]
+            for r in range(n):
+                src[r].copy_(torch.from_numpy(data[r]).cuda())
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            for c in comms:
+                c.sync()
+            exp = np.concatenate(data)
+            for r in range(n):
+                assert np.array_equal(out[r].cpu().numpy(), exp), (it, r)
+        _algo(comms, "oneshot")
+    finally:
+        torch.cuda.synchronize()
+        vnode.destroy(comms)

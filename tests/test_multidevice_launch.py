@@ -413,3 +413,26 @@ def test_direct_default_thresholds(fake, monkeypatch, n, oneshot, direct):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_allgather_oneshot_plans(fake):
+    """AllGather buckets up to oneshot_bytes per rank take the direct kernel's
+    AllGather mode; larger ones the ring."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(oneshot_bytes=64 << 10, direct_bytes=-1))
+    try:
+        for nbytes, kind, algo in ((1000, "direct", "oneshot"), (65536, "direct", "oneshot"), (65537, "ring", "ring")):
+            _log()
+            with C.group():
+                for r, c in enumerate(comms):
+                    C.all_gather(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, nbytes, stream=0)
+            launches = [kv for k, kv in _log() if k == "launch"]
+            assert [kv["kind"] for kv in launches] == [kind] * 8
+            if kind == "direct":
+                assert all(kv["mode"] == "ag-oneshot" and int(kv["count"]) == nbytes for kv in launches)
+            assert [c.last_algo() for c in comms] == [algo] * 8
+        for c in comms:
+            c.sync()
+    finally:
+        for c in comms:
+            c.destroy()
