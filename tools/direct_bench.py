@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--calls", type=int, default=100)
     ap.add_argument("--dtype", default="float16")
     ap.add_argument("--oneshot-max-kib", type=int, default=2048)
+    ap.add_argument("--allgather", action="store_true", help="time AllGather (size = bytes per rank): ring vs one-shot")
     args = ap.parse_args()
     dt = getattr(torch, args.dtype)
     code = {torch.float16: 6, torch.float32: 7, torch.bfloat16: 9}[dt]
@@ -47,10 +48,12 @@ def main():
         for kib in args.sizes_kib:
             cnt = (kib << 10) // es
             xs = [torch.randn(cnt, device="cuda").to(dt) for _ in range(n)]
-            ys = [torch.empty_like(x) for x in xs]
+            ys = [torch.empty(n * cnt if args.allgather else cnt, dtype=dt, device="cuda") for _ in xs]
             row = {"n": n, "bytes": kib << 10}
             for algo, comms in sets.items():
                 if algo == "oneshot" and kib > args.oneshot_max_kib:
+                    continue
+                if args.allgather and algo == "direct":
                     continue
                 for blocks in (args.blocks if algo != "ring" else [0]):
                     if blocks:
@@ -59,7 +62,10 @@ def main():
                     def once():
                         with C.group():
                             for r in range(n):
-                                C.all_reduce(comms[r], xs[r], ys[r], cnt, code, 0, stream=st)
+                                if args.allgather:
+                                    C.all_gather(comms[r], xs[r], ys[r], cnt * es, stream=st)
+                                else:
+                                    C.all_reduce(comms[r], xs[r], ys[r], cnt, code, 0, stream=st)
 
                     for _ in range(5):
                         once()
@@ -94,7 +100,8 @@ def main():
         for comms in sets.values():
             for c in comms:
                 c.destroy()
-    print(json.dumps({"tool": "direct_bench", "dtype": args.dtype, "rows": rows}), flush=True)
+    print(json.dumps({"tool": "direct_bench", "collective": "allgather" if args.allgather else "allreduce",
+                      "dtype": args.dtype, "rows": rows}), flush=True)
 
 
 if __name__ == "__main__":
