@@ -43,9 +43,10 @@ def main():
         sys.exit("this libmccs_hip.so has no direct trace: build it with -DMCCS_DIRECT_TRACE")
     rows = []
     for n in a.n:
-        for variant, kw in (("direct", dict(direct_bytes=8 << 20, oneshot_bytes=-1)),
-                            ("direct-cached", dict(direct_bytes=8 << 20, oneshot_bytes=-1, fifo_memory=C.FIFO_DEVICE)),
-                            ("oneshot", dict(direct_bytes=-1, oneshot_bytes=8 << 20))):
+        cap = max(a.kib) << 10
+        for variant, kw in (("direct", dict(direct_bytes=cap, oneshot_bytes=-1)),
+                            ("direct-cached", dict(direct_bytes=cap, oneshot_bytes=-1, fifo_memory=C.FIFO_DEVICE)),
+                            ("oneshot", dict(direct_bytes=-1, oneshot_bytes=min(cap, 64 << 20)))):
             comms = C.init_all([0] * n, C.CommConfig(**kw))
             for kib in a.kib:
                 cnt = (kib << 10) // 2
