@@ -241,7 +241,9 @@ class FakeRuntime final : public DeviceRuntime {
                 " mode=" + (da->mode == MCCS_DIRECT_ONE_SHOT      ? "oneshot"
                             : da->mode == MCCS_DIRECT_AG_ONE_SHOT ? "ag-oneshot"
                                                                   : "twoshot") +
-                " piece=" + std::to_string(da->piece) + " piece2=" + std::to_string(da->piece2);
+                " piece=" + std::to_string(da->piece) + " piece2=" + std::to_string(da->piece2) + " owned=";
+        for (unsigned t = 0; t < da->nranks && t < MCCS_DIRECT_MAX_RANKS; ++t)
+          extra += (t ? "," : "") + std::to_string(da->owned[t]);
       } else {
         const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
         for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(ma->comm[k]) == cur_;

@@ -436,3 +436,35 @@ def test_allgather_oneshot_plans(fake):
     finally:
         for c in comms:
             c.destroy()
+
+
+@pytest.mark.parametrize("n,count,rings", [(8, 1 << 20, None), (8, 3_000_001, None), (4, 777, None),
+                                           (3, 1_234_567, None), (8, 2_500_000, "doubled")])
+def test_direct_ownership_matches_the_oracle(fake, orc, n, count, rings):
+    """The host's per-rank element counts (the kernel's hand-off thresholds)
+    equal the oracle's chunk ownership for the same walk (channels, threads,
+    rings, 4 MiB FIFO buffer), including multi-loop walks and 2 x channels."""
+    import numpy as np
+
+    fake(n)
+    ring_list = None
+    if rings == "doubled":
+        base = C.default_rings(n, 0)
+        ring_list = base + [list(reversed(r)) for r in base]
+    comms = C.init_all(list(range(n)), C.CommConfig(direct_bytes=64 << 20, oneshot_bytes=-1, rings=ring_list))
+    try:
+        _log()
+        _allreduce_group(comms, count=count)
+        launches = [kv for k, kv in _log() if k == "launch"]
+        assert launches and all(kv["mode"] == "twoshot" for kv in launches)
+        owned = [int(v) for v in launches[0]["owned"].split(",")]
+        nch, nthr = C.task_schema(count * 4, comms[0].nchannels)
+        zeros = [np.zeros(count, np.float32) for _ in range(n)]
+        _, owner = orc.ring_allreduce(7, 0, zeros, nchannels=nch, nthreads=nthr, ring_orders=comms[0].rings()[:nch],
+                                      want_owner=True)
+        assert owned == np.bincount(owner, minlength=n).tolist()
+        for c in comms:
+            c.sync()
+    finally:
+        for c in comms:
+            c.destroy()
