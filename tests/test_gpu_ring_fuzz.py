@@ -2,7 +2,8 @@
 
 Each case draws the rank count, dtype, op, element count (ragged, sometimes
 tiny, sometimes several FIFO loops), channels, lanes, block size, FIFO depth, FIFO
-memory kind, data placement, slicing and an optional ring override, runs one
+memory kind, data placement, slicing, an optional ring override and, half of
+the time, direct-kernel thresholds and workgroup caps, runs one
 grouped AllReduce (or AllGather) on a virtual node and compares every rank
 bit for bit with the oracle's restatement of the reference schedule.
 """
@@ -47,12 +48,21 @@ def _case(seed):
     if rng.random() < 0.3:
         cfg["fifo_slots"] = int(rng.choice([16, 32]))
     fifo_works = bool(rng.random() < 0.3)  # work list through the FIFO even where it fits the launch arguments
-    return n, code, op, count, cfg, slice2, gather, fifo_works, rng
+    # the direct kernel (one-shot / two-shot / AllGather one-shot) at random
+    # thresholds and workgroup caps; results must not change
+    blocks = None
+    if rng.random() < 0.5:
+        cfg["oneshot_bytes"] = int(rng.choice([-1, 64 << 10, 1 << 20, 8 << 20]))
+        cfg["direct_bytes"] = int(rng.choice([-1, 1 << 20, 8 << 20, 32 << 20]))
+        blocks = int(rng.choice([1, 3, 16, 128]))
+    return n, code, op, count, cfg, slice2, gather, fifo_works, blocks, rng
 
 
 @pytest.mark.parametrize("seed", range(CASES))
 def test_random_ring_case(orc, seed, monkeypatch):
-    n, code, op, count, cfg, slice2, gather, fifo_works, rng = _case(1000 + seed)
+    n, code, op, count, cfg, slice2, gather, fifo_works, blocks, rng = _case(1000 + seed)
+    if blocks:
+        monkeypatch.setenv("MCCS_DIRECT_BLOCKS", str(blocks))
     if slice2:
         monkeypatch.setenv("MCCS_SLICE_STEPS", "2")
     if fifo_works:
