@@ -498,10 +498,16 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   const size_t bytes = nbytes;
   // two-shot phases 1 and 3: the chunks others own; AllGather phase 2: n-1 segments
   const size_t scatter = gather ? bytes * (n - 1) : oneshot ? bytes : bytes - bytes / n;
+  // Ranks sharing a GPU split its CUs: at most one direct workgroup per CU
+  // per rank (the virtual node ran n = 4 / 8 fastest at 64 / 32 workgroups
+  // per rank, i.e. one per CU in all; two per CU cost up to 1.5x), and never
+  // more than can be resident at once (they spin on each other's counts).
   const int cap = coresident_direct_blocks(c0->device);
+  int ncu = 0;
+  if (rt().CuCount(&ncu, c0->device) != hipSuccess || ncu <= 0) ncu = cap;
   long g = std::min<long>((long)((scatter + 8191) / 8192), direct_max_blocks());
-  if (idx.size() > 1) g = std::min<long>(g, cap / (long)idx.size());  // one fused launch: co-scheduled
-  else if (c0->share > 1) g = std::min<long>(g, cap / 2 / c0->share);  // separate processes: half the slots
+  if (idx.size() > 1) g = std::min<long>(g, std::min(cap, ncu) / (long)idx.size());  // one fused launch
+  else if (c0->share > 1) g = std::min<long>(g, std::min(cap / 2, ncu) / c0->share);  // separate processes
   g = std::max<long>(g, 1);
   if (g * (long)idx.size() > cap) {
     MCCS_LOG("direct launch of %zu ranks x %ld workgroups exceeds the %d co-resident ones of device %d", idx.size(),
