@@ -50,6 +50,9 @@
 
 namespace mccs {
 
+#ifndef MCCS_DIRECT_SCALAR_PTRS
+#define MCCS_DIRECT_SCALAR_PTRS 1
+#endif
 #ifndef MCCS_DIRECT_UNROLL
 #define MCCS_DIRECT_UNROLL 2
 #endif
@@ -232,12 +235,19 @@ __device__ __forceinline__ void direct_reduce(const void* const* src_in, int n, 
   void* dst[MCCS_DIRECT_MAX_RANKS];
 #pragma unroll
   for (int j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j) {
+#if MCCS_DIRECT_SCALAR_PTRS
     src[j] = (const void*)uniform_u64((uint64_t)src_in[j]);
     dst[j] = (void*)uniform_u64((uint64_t)dst_in[j]);
+#else
+    src[j] = src_in[j];
+    dst[j] = dst_in[j];
+#endif
   }
+#if MCCS_DIRECT_SCALAR_PTRS
   ne = (int64_t)uniform_u64((uint64_t)ne);
   n = __builtin_amdgcn_readfirstlane(n);
   ndst = __builtin_amdgcn_readfirstlane(ndst);
+#endif
   uintptr_t mis = 0;
 #pragma unroll
   for (int j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j) {

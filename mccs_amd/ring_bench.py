@@ -14,7 +14,8 @@ Correctness gates (any failure exits non-zero, no line is printed):
     dtype, bit for bit on every rank, for every transport candidate;
   * after timing: the full-size exact-sum AllReduce again;
   * every extra leg (fp16 1 GiB, AllGather, size sweep, configs[4] jobs)
-    validates its own results.
+    validates its own results; the direct-kernel sweep (one-shot / two-shot
+    beside the ring) records a failing variant instead of failing the line.
 A transport candidate is skipped when its communicator cannot be created
 (e.g. IPC refuses to export that memory kind) or when it fails the gate
 BEFORE timing (a wrong sum or a device watchdog in the uncached-FIFO mode on
@@ -28,6 +29,8 @@ from __future__ import annotations
 import os
 import subprocess
 import time
+
+from ._streams import side_stream
 
 XGMI_LINK_GBPS_PER_DIR = 76.8  # MI355X xGMI per link per direction (spec); see DESIGN.md
 HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
@@ -259,7 +262,6 @@ def shared_gpu_lanes(world: int) -> int:
 def graph_replay(torch, dist, comm, call_on, calls=10):
     """Per-call time of `calls` AllReduces captured in one HIP graph (max over
     ranks), after one untimed replay.  call_on(stream) issues one AllReduce."""
-    from ._streams import side_stream
 
     torch.cuda.synchronize()
     gs = side_stream(torch, slot=1)  # one graph stream per process (mccs_amd/_streams.py)
@@ -372,9 +374,6 @@ def size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20, graph_upt
             row["graph_latency_us"] = round(gl * 1e6, 2)
         rows.append(row)
     return rows
-
-
-from ._streams import side_stream  # noqa: E402
 
 
 def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, ring_rows, upto=8 << 20,
@@ -848,7 +847,6 @@ def setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup
                                      modes, (count, torch.float16, C.AllReduceDataType.Float16), grp)
     if comm is None:
         raise BenchFailure(f"{name}: communicator creation failed")
-    from ._streams import side_stream
 
     stream = side_stream(torch, device, slot=1)
     tj = traffic.TraceJob(torch, name, [comm], [jrank], half, count, compute_us * 1e-6 * compute_scale, stream, dev)
