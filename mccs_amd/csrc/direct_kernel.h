@@ -50,9 +50,6 @@
 
 namespace mccs {
 
-#ifndef MCCS_DIRECT_SCALAR_PTRS
-#define MCCS_DIRECT_SCALAR_PTRS 1
-#endif
 #ifndef MCCS_DIRECT_UNROLL
 #define MCCS_DIRECT_UNROLL 2
 #endif
@@ -214,40 +211,18 @@ __device__ __forceinline__ void direct_count_out(DirectShm& sh, const mccsDirect
   __syncthreads();
 }
 
-__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // acc = x[src0]; acc = fn(x[srcj], acc) (j = 1..n-1) over the sources in
 // ring order, stored to every non-null destination among dst[0 .. ndst)
 // (n = 1: a copy to several places).
 template <int DT, int OP>
-__device__ __forceinline__ void direct_reduce(const void* const* src_in, int n, void* const* dst_in, int ndst,
-                                              int64_t ne) {
+// (Forcing the uniform pointers into scalar registers with readfirstlane
+// cut VGPRs from ~160 to ~113 and ran 3-7 % slower on the virtual node: the
+// second resident workgroup per CU it allows costs more than it gives.)
+__device__ __forceinline__ void direct_reduce(const void* const* src, int n, void* const* dst, int ndst, int64_t ne) {
   using T = typename Elem<DT>::T;
   constexpr int PACK = kPackElems<DT>;
   constexpr int U = kElemBytes<DT> == 1 ? 1 : kDirectUnroll;  // byte types unpack 16 lanes per pack
   const int tid = threadIdx.x, nthr = blockDim.x;
-  // the pointers are the workgroup's (uniform): keep them in scalar registers
-  const void* src[MCCS_DIRECT_MAX_RANKS];
-  void* dst[MCCS_DIRECT_MAX_RANKS];
-#pragma unroll
-  for (int j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j) {
-#if MCCS_DIRECT_SCALAR_PTRS
-    src[j] = (const void*)uniform_u64((uint64_t)src_in[j]);
-    dst[j] = (void*)uniform_u64((uint64_t)dst_in[j]);
-#else
-    src[j] = src_in[j];
-    dst[j] = dst_in[j];
-#endif
-  }
-#if MCCS_DIRECT_SCALAR_PTRS
-  ne = (int64_t)uniform_u64((uint64_t)ne);
-  n = __builtin_amdgcn_readfirstlane(n);
-  ndst = __builtin_amdgcn_readfirstlane(ndst);
-#endif
   uintptr_t mis = 0;
 #pragma unroll
   for (int j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j) {
