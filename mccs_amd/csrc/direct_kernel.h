@@ -138,6 +138,7 @@ struct DirectShm {
   char* region[MCCS_DIRECT_MAX_RANKS];                          // me.region
   uint64_t seq;
   uint64_t e_in;                            // E_IN at launch start
+  uint64_t e_self;                          // E_SELF at launch start
   uint64_t e_out[MCCS_DIRECT_MAX_RANKS];    // E_OUT at launch start
   uint64_t owned[MCCS_DIRECT_MAX_RANKS];    // elements of this launch's chunks each rank owns
   uint64_t sent[MCCS_DIRECT_MAX_RANKS];     // elements this workgroup wrote into each rank's slots (this phase)
@@ -191,9 +192,10 @@ __device__ __forceinline__ bool direct_wait(DirectShm& sh, const char* ctrl, int
 // This workgroup's writes of the phase are complete (and, for cached arenas,
 // written back): add what it wrote into each rank's slots (sh.sent) to that
 // rank's count line for this rank (lane t of wave 0 for rank t: one remote
-// atomic each, no return value awaited), then clear sh.sent.
+// atomic each, no return value awaited), then clear sh.sent.  self: also
+// count sh.sent[me] into this rank's own line (its reads of the input done).
 __device__ __forceinline__ void direct_count_out(DirectShm& sh, const mccsDirectArgs& a, const mccsDirectRank& me,
-                                                 int cnt_base) {
+                                                 int cnt_base, bool self = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < 64 && sh.ok) {
@@ -202,7 +204,7 @@ __device__ __forceinline__ void direct_count_out(DirectShm& sh, const mccsDirect
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     const uint32_t t = threadIdx.x;
-    if (t < a.nranks && t != me.rank && sh.sent[t])
+    if (t < a.nranks && (t != me.rank || self) && sh.sent[t])
       __hip_atomic_fetch_add((uint64_t*)(sh.region[t] + cnt_base + (int)me.rank * MCCS_FLAG_LINE_BYTES), sh.sent[t],
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -214,10 +216,10 @@ __device__ __forceinline__ void direct_count_out(DirectShm& sh, const mccsDirect
 // acc = x[src0]; acc = fn(x[srcj], acc) (j = 1..n-1) over the sources in
 // ring order, stored to every non-null destination among dst[0 .. ndst)
 // (n = 1: a copy to several places).
-template <int DT, int OP>
 // (Forcing the uniform pointers into scalar registers with readfirstlane
 // cut VGPRs from ~160 to ~113 and ran 3-7 % slower on the virtual node: the
 // second resident workgroup per CU it allows costs more than it gives.)
+template <int DT, int OP>
 __device__ __forceinline__ void direct_reduce(const void* const* src, int n, void* const* dst, int ndst, int64_t ne) {
   using T = typename Elem<DT>::T;
   constexpr int PACK = kPackElems<DT>;
@@ -280,6 +282,13 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   const DirectWalk w = direct_walk<DT>(a);
   const bool ag = a.mode == MCCS_DIRECT_AG_ONE_SHOT;  // AllGather: bytes, no reduction
   const bool one_shot = a.mode == MCCS_DIRECT_ONE_SHOT || ag;
+  // In-place one-shot AllReduce: phase 2 overwrites the input that other
+  // workgroups of this rank may still be reading in phase 1 (their pieces
+  // differ), so phase 2 also waits for this rank's own workgroups to have
+  // counted their reads (IN_CNT(me), E_SELF).  AllGather in place writes
+  // only the other ranks' segments in phase 2; two-shot pieces keep a
+  // workgroup on the same bytes in phases 1 and 3.
+  const bool self_wait = a.mode == MCCS_DIRECT_ONE_SHOT && me.send == me.recv;
   MCCS_DTRACE(kDtStart);
   // Prologue: lanes of wave 0 load the state words (and the abort flag) in
   // one round trip.
@@ -292,7 +301,8 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
       v = abort_raised(abortFlag) ? 1 : 0;
     if (lane == MCCS_DIRECT_ST_LAUNCHES) sh.seq = v + 1;
     if (lane == MCCS_DIRECT_ST_E_IN) sh.e_in = v;
-    if (lane >= 2 && lane < MCCS_DIRECT_ST_WORDS) sh.e_out[lane - 2] = v;
+    if (lane >= 2 && lane < 2 + MCCS_DIRECT_MAX_RANKS) sh.e_out[lane - 2] = v;
+    if (lane == MCCS_DIRECT_ST_E_SELF) sh.e_self = v;
     if (lane == MCCS_DIRECT_ST_WORDS) sh.ok = v == 0;
     if (lane < MCCS_DIRECT_MAX_RANKS) {
       sh.owned[lane] = a.owned[lane];
@@ -333,6 +343,9 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
         for (int t = 0; t < n; ++t)
           __hip_atomic_store(st + MCCS_DIRECT_ST_E_OUT(t), sh.e_out[t] + sh.owned[t], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+      if (self_wait)
+        __hip_atomic_store(st + MCCS_DIRECT_ST_E_SELF, sh.e_self + (uint64_t)w.size, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(st + MCCS_DIRECT_ST_LAUNCHES, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
@@ -361,11 +374,13 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
         for (int t = 0; t < n; ++t) sh.sent[t] += (uint64_t)ne;
     }
     MCCS_DTRACE(kDtPhase1);
-    direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0));
+    direct_count_out(sh, a, me, MCCS_DIRECT_IN_CNT(0), self_wait);
     MCCS_DTRACE(kDtCounted1);
     advance();
-    if (threadIdx.x < MCCS_DIRECT_MAX_RANKS) need[threadIdx.x] = sh.e_in + (uint64_t)w.size;
+    if (threadIdx.x < MCCS_DIRECT_MAX_RANKS)
+      need[threadIdx.x] = (threadIdx.x == me.rank ? sh.e_self : sh.e_in) + (uint64_t)w.size;
     __syncthreads();
+    const uint32_t waitmask = self_wait ? peers | (1u << me.rank) : peers;
     bool in_seen = false;  // uniform across the workgroup
     if (ag) {
       // 2. (AllGather) every peer's segment, from its slot to the output;
@@ -395,7 +410,7 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
                   [&](int64_t off, int64_t ne, int bid, int k, uint32_t) {
                     if (!sh.ok) return;
                     if (!in_seen) {
-                      if (!direct_wait(sh, mine, MCCS_DIRECT_IN_CNT(0), peers, need, abortFlag, a, ecfg)) return;
+                      if (!direct_wait(sh, mine, MCCS_DIRECT_IN_CNT(0), waitmask, need, abortFlag, a, ecfg)) return;
                       in_seen = true;
                       MCCS_DTRACE(kDtWait2);
                     }

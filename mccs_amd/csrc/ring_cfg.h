@@ -136,7 +136,9 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 //     s+1, made after this rank finished reading parity p in launch s.
 #define MCCS_DIRECT_MAX_RANKS 8
 #define MCCS_DIRECT_CTRL_BYTES 65536
-#define MCCS_DIRECT_IN_CNT(s) ((s) * MCCS_FLAG_LINE_BYTES)             // u64, added to by sender s
+// u64, added to by sender s; a rank's own line IN_CNT(rank) counts its own
+// workgroups' reads of an in-place one-shot input (nobody else writes it)
+#define MCCS_DIRECT_IN_CNT(s) ((s) * MCCS_FLAG_LINE_BYTES)
 #define MCCS_DIRECT_OUT_CNT(o) (1024 + (o) * MCCS_FLAG_LINE_BYTES)     // u64, added to by owner o
 // u64 state words (one line, read by one wave load): launches completed,
 // E_IN (elements each sender has sent so far), E_OUT[o] (elements owner o
@@ -145,7 +147,8 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 #define MCCS_DIRECT_ST_LAUNCHES 0
 #define MCCS_DIRECT_ST_E_IN 1
 #define MCCS_DIRECT_ST_E_OUT(o) (2 + (o))
-#define MCCS_DIRECT_ST_WORDS (2 + MCCS_DIRECT_MAX_RANKS)
+#define MCCS_DIRECT_ST_E_SELF (2 + MCCS_DIRECT_MAX_RANKS)  // elements this rank counted to itself (in-place one-shot)
+#define MCCS_DIRECT_ST_WORDS (3 + MCCS_DIRECT_MAX_RANKS)
 #define MCCS_DIRECT_DONE 4096                                          // u32: workgroups arrived in the launch
 #define MCCS_DIRECT_SLOTS (MCCS_DIRECT_MAX_RANKS + 1)                  // two-shot slots
 #define MCCS_DIRECT_THREADS 512
