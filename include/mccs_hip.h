@@ -135,14 +135,14 @@ typedef struct {
                            (two-shot) kernel on a fully connected node of <= 8 ranks: every chunk to
                            its ring owner, reduced in the ring's order, results broadcast, so the
                            output equals the ring's bit for bit; larger buckets take the ring.
-                           0 = default (MCCS_DIRECT_BYTES; else 4 MiB at >= 4 ranks, off below),
+                           0 = default (MCCS_DIRECT_BYTES; else 4 MiB at >= 3 ranks, off at 2),
                            < 0 = never.  Every rank must agree
                            (it sizes the arena: Connect refuses a mismatch) */
   int oneshot_bytes;    /* buckets of at most this many bytes per rank take the one-shot variant
                            instead: every rank sends its whole input to every peer and reduces
                            every chunk itself (same order, same bits; one exchange instead of
-                           two).  0 = default (MCCS_ONESHOT_BYTES; else 1 MiB at <= 4 ranks, 256 KiB
-                           above), < 0 = never; ranks must agree */
+                           two).  0 = default (MCCS_ONESHOT_BYTES; else 2 MiB at 2 ranks, 1 MiB at
+                           3-4, 256 KiB above), < 0 = never; ranks must agree */
 } mccsCommConfig;
 
 void mccsCommConfigDefault(mccsCommConfig *cfg);

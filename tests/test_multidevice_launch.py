@@ -329,8 +329,8 @@ def test_direct_allreduce_plans(fake):
 
 
 def test_direct_defaults_and_fused_ranks(fake, monkeypatch):
-    """Library defaults at n = 2: one-shot up to 1 MiB, the ring above
-    (two-shot off below 4 ranks); fused ranks on one device share one direct
+    """Library defaults at n = 2: one-shot up to 2 MiB, the ring above
+    (two-shot off at 2 ranks); fused ranks on one device share one direct
     launch; without peer atomics every AllReduce takes the ring."""
     for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES"):
         monkeypatch.delenv(k, raising=False)
@@ -347,7 +347,7 @@ def test_direct_defaults_and_fused_ranks(fake, monkeypatch):
             c.sync()
         plain = C.init_all([0, 1])
         assert all(c.direct_enabled() for c in plain)
-        for count, want in ((1000, "oneshot"), (262144, "oneshot"), (262145, "ring")):
+        for count, want in ((1000, "oneshot"), (524288, "oneshot"), (524289, "ring")):
             _log()
             _allreduce_group(plain, count=count)
             assert [kv["kind"] for k, kv in _log() if k == "launch"] == (["direct"] * 2 if want != "ring" else
@@ -395,7 +395,8 @@ def test_oneshot_below_its_threshold(fake):
             c.destroy()
 
 
-@pytest.mark.parametrize("n,oneshot,direct", [(4, 1 << 20, 4 << 20), (8, 256 << 10, 4 << 20), (3, 1 << 20, None)])
+@pytest.mark.parametrize("n,oneshot,direct", [(4, 1 << 20, 4 << 20), (8, 256 << 10, 4 << 20), (3, 1 << 20, 4 << 20),
+                                              (2, 2 << 20, None)])
 def test_direct_default_thresholds(fake, monkeypatch, n, oneshot, direct):
     for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES"):
         monkeypatch.delenv(k, raising=False)
