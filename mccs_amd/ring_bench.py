@@ -376,7 +376,7 @@ def size_sweep(torch, dist, C, comm, rank, world, dev, warmup=3, K=20, graph_upt
     return rows
 
 
-def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, ring_rows, upto=8 << 20,
+def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, ring_rows, upto=32 << 20,
                  oneshot_upto=2 << 20, warmup=3, K=20):
     """The direct AllReduce variants (direct_kernel.h) beside the ring over the
     sweep's sizes up to `upto`: two-shot and one-shot communicators built with
