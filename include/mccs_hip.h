@@ -248,6 +248,10 @@ mccsResult_t mccs_host_ring_allreduce(int nranks, const void *const *sendbufs, v
 /* Default ring orders for an n-rank node (edge-disjoint Hamiltonian cycles,
  * both directions); writes up to max_channels x nranks ints, returns count. */
 int mccs_default_rings(int nranks, int nch_req, int *out, int max_channels);
+/* The library's default direct thresholds for an n-rank communicator (what
+ * mccsCommConfig.oneshot_bytes / direct_bytes = 0 resolve to without the
+ * MCCS_* overrides; -1 = off). */
+void mccs_direct_defaults(int nranks, int *oneshot_bytes, int *direct_bytes);
 /* get_task_schema (plan.rs:602-635): channels and threads for total_bytes. */
 void mccs_task_schema(size_t total_bytes, int nch_cfg, int *nch, int *nthreads);
 

@@ -124,6 +124,7 @@ SIGNATURES: dict[str, tuple] = {
     "mccsGetErrorString": (ctypes.c_char_p, [_c_int]),
     "mccs_default_rings": (_c_int, [_c_int, _c_int, _P(_c_int), _c_int]),
     "mccs_task_schema": (None, [_c_size_t, _c_int, _P(_c_int), _P(_c_int)]),
+    "mccs_direct_defaults": (None, [_c_int, _P(_c_int), _P(_c_int)]),
     "mccs_host_ring_allreduce": (
         _c_int, [_c_int, _P(_c_void_p), _P(_c_void_p), _c_size_t, _c_int, _c_int, _c_int, _c_int, _c_int,
                  _P(_c_int)]),

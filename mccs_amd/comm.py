@@ -283,6 +283,14 @@ def ring_profile(device: int = 0, reset: bool = True) -> dict:
             "drain_us": out[3] / n / 100.0}
 
 
+def direct_defaults(nranks: int) -> tuple[int, int]:
+    """(oneshot_bytes, direct_bytes) the library uses by default for n ranks
+    (-1 = off); host-only."""
+    a, b = _ci(), _ci()
+    _sig().mccs_direct_defaults(int(nranks), ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
 def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
     a, b = _ci(), _ci()
     _sig().mccs_task_schema(total_bytes, channels, ctypes.byref(a), ctypes.byref(b))
@@ -291,5 +299,6 @@ def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
 
 __all__ = ["AllReduceDataType", "AllReduceOpType", "CommConfig", "Communicator", "init_all",
            "init_communicator_rank", "all_reduce", "all_gather", "group", "default_rings", "task_schema",
+           "direct_defaults",
            "host_ring_allreduce", "ring_profile",
            "RedOp", "DataType"]

@@ -511,6 +511,11 @@ extern "C" int mccs_default_rings(int nranks, int nch_req, int* out, int max_cha
   return n;
 }
 
+extern "C" void mccs_direct_defaults(int nranks, int* oneshot_bytes, int* direct_bytes) {
+  if (oneshot_bytes) *oneshot_bytes = default_oneshot_bytes(nranks);
+  if (direct_bytes) *direct_bytes = default_direct_bytes(nranks);
+}
+
 extern "C" void mccs_task_schema(size_t total_bytes, int nch_cfg, int* nch, int* nthreads) {
   task_schema(total_bytes, nch_cfg, nch, nthreads);
 }

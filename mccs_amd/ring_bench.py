@@ -465,6 +465,15 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
         wins = [r["bytes"] for r in out["rows"] if f"{algo}_graph_us" in r and "ring_graph_us" in r
                 and r[f"{algo}_graph_us"] < r["ring_graph_us"]]
         best[f"{algo}_beats_ring_upto_bytes"] = max(wins) if wins else 0
+    # what the library's defaults pick at each size (thresholds of api.cpp)
+    os_b, d_b = C.direct_defaults(world)
+    best["default_thresholds"] = {"oneshot_bytes": os_b, "direct_bytes": d_b}
+    for r in out["rows"]:
+        nb = r["bytes"]
+        pick = ("oneshot" if 0 < nb <= os_b else "direct" if 0 < nb <= d_b else "ring")
+        if not out["p2p_atomics"] or f"{pick}_graph_us" not in r and pick != "ring":
+            pick = "ring"
+        r["default_algo"] = pick
     out["summary"] = best
     if dead:
         out["failed"] = dead

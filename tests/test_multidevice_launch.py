@@ -400,6 +400,7 @@ def test_oneshot_below_its_threshold(fake):
 def test_direct_default_thresholds(fake, monkeypatch, n, oneshot, direct):
     for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES"):
         monkeypatch.delenv(k, raising=False)
+    assert C.direct_defaults(n) == (oneshot, direct or -1)
     fake(n)
     comms = C.init_all(list(range(n)))
     try:
