@@ -135,7 +135,8 @@ typedef struct {
                            (two-shot) kernel on a fully connected node of <= 8 ranks: every chunk to
                            its ring owner, reduced in the ring's order, results broadcast, so the
                            output equals the ring's bit for bit; larger buckets take the ring.
-                           0 = default (MCCS_DIRECT_BYTES; else 4 MiB at >= 3 ranks, off at 2),
+                           0 = default (MCCS_DIRECT_BYTES; else 8 MiB at >= 4 ranks, 4 MiB at 3,
+                           off at 2),
                            < 0 = never.  Every rank must agree
                            (it sizes the arena: Connect refuses a mismatch) */
   int oneshot_bytes;    /* buckets of at most this many bytes per rank take the one-shot variant

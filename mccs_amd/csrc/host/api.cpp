@@ -37,14 +37,14 @@ static void group_discard() {
 // the one-shot / two-shot kernel (bit-identical to the ring either way).
 // Virtual node, graph replay, fp16 (profiles/r03_direct_vnode*.json): one-shot
 // beat the ring to 2 MiB at n = 2, and beat two-shot to ~1 MiB at n = 3 / 4
-// and to 512 KiB at n = 8; two-shot beat the ring to 2-8 MiB at n = 3 / 4 / 8
-// and only tied it at n = 2 (where the ring is already two hops).  Over xGMI
+// and to 512 KiB at n = 8; two-shot beat the ring to 2 MiB at n = 3 and to
+// 8 MiB at n = 4 / 8 and only tied it at n = 2 (the ring is two hops there).  Over xGMI
 // the ring's 2(n-1) sequential hops cost more than here, so these are
 // conservative; the node's sweep (bench config.direct_sweep_fp16) refines them.
 static int default_oneshot_bytes(int nranks) {
   return nranks == 2 ? 2 << 20 : nranks <= 4 ? 1 << 20 : 256 << 10;
 }
-static int default_direct_bytes(int nranks) { return nranks >= 3 ? 4 << 20 : -1; }
+static int default_direct_bytes(int nranks) { return nranks >= 4 ? 8 << 20 : nranks == 3 ? 4 << 20 : -1; }
 
 static void fill_defaults(mccsCommConfig* c, int nranks) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19

@@ -312,14 +312,14 @@ def test_direct_hand_off_modes(orc, fifo, variant):
 
 def test_library_defaults(orc):
     """The library defaults at n = 4: one-shot up to 1 MiB per rank, two-shot
-    up to 4 MiB, the ring above."""
+    up to 8 MiB, the ring above."""
     n = 4
     comms = C.init_all([0] * n)
     try:
         assert all(c.direct_enabled() for c in comms)
         rng = np.random.default_rng(44)
-        for count, want in ((1000, "oneshot"), (262144, "oneshot"), (262145, "direct"), (1 << 20, "direct"),
-                            ((1 << 20) + 1, "ring")):
+        for count, want in ((1000, "oneshot"), (262144, "oneshot"), (262145, "direct"), (2 << 20, "direct"),
+                            ((2 << 20) + 1, "ring")):
             inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
             outs = vnode.run_allreduce(comms, inputs, F32, 0)
             _algo(comms, want)

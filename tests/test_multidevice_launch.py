@@ -395,7 +395,7 @@ def test_oneshot_below_its_threshold(fake):
             c.destroy()
 
 
-@pytest.mark.parametrize("n,oneshot,direct", [(4, 1 << 20, 4 << 20), (8, 256 << 10, 4 << 20), (3, 1 << 20, 4 << 20),
+@pytest.mark.parametrize("n,oneshot,direct", [(4, 1 << 20, 8 << 20), (8, 256 << 10, 8 << 20), (3, 1 << 20, 4 << 20),
                                               (2, 2 << 20, None)])
 def test_direct_default_thresholds(fake, monkeypatch, n, oneshot, direct):
     for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES"):
