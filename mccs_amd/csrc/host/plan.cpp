@@ -491,7 +491,7 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
                             ? 0
                             : std::max(da->timeout_ticks, ck->kcfg.timeout_ticks);
   }
-  // Workgroups: ~8 KiB of phase-1 bytes each at least, at most
+  // Workgroups: ~4 KiB of phase-1 bytes each at least, at most
   // MCCS_DIRECT_BLOCKS; pieces: each phase's bytes over the workgroups, in
   // 4 KiB steps (aligned: chunk offsets are granule multiples), 4..64 KiB.
   // One-shot: phase 1 sends the whole input, phase 2 reduces all of it.
@@ -505,7 +505,15 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   const int cap = coresident_direct_blocks(c0->device);
   int ncu = 0;
   if (rt().CuCount(&ncu, c0->device) != hipSuccess || ncu <= 0) ncu = cap;
-  long g = std::min<long>((long)((scatter + 8191) / 8192), direct_max_blocks());
+  // scatter bytes per workgroup (MCCS_DIRECT_WG_BYTES): 4 KiB beat 8 / 16 KiB
+  // on the virtual node at 32-512 KiB (n = 8 32 KiB one-shot 19.1 -> 14.4 us,
+  // 16 KiB: 27.0) and tied 2 KiB (pieces are >= 4 KiB)
+  static const long wg_bytes = [] {
+    const char* v = std::getenv("MCCS_DIRECT_WG_BYTES");
+    const long x = v ? std::atol(v) : 0;
+    return x >= 1024 ? x : 4096L;
+  }();
+  long g = std::min<long>((long)((scatter + wg_bytes - 1) / wg_bytes), direct_max_blocks());
   if (idx.size() > 1) g = std::min<long>(g, std::min(cap, ncu) / (long)idx.size());  // one fused launch
   else if (c0->share > 1) g = std::min<long>(g, std::min(cap / 2, ncu) / c0->share);  // separate processes
   g = std::max<long>(g, 1);
