@@ -375,13 +375,16 @@ int coresident_ring_blocks(int block, int device) {
 // Workgroups of the direct kernels the device holds at once (min over the
 // instantiations): a direct launch spins on peers' flags, so all of its
 // workgroups, and those of ranks sharing the GPU, must be resident together.
-static int coresident_direct_blocks(int device) {
+static int coresident_direct_blocks(int device, int* ncu_out = nullptr) {
   static std::mutex mu;
-  static std::map<int, int> cache;
+  static std::map<int, std::pair<int, int>> cache;  // device -> (blocks, CUs)
   {
     std::lock_guard<std::mutex> lk(mu);
     auto it = cache.find(device);
-    if (it != cache.end()) return it->second;
+    if (it != cache.end()) {
+      if (ncu_out) *ncu_out = it->second.second;
+      return it->second.first;
+    }
   }
   DeviceGuard g(device);
   int ncu = 0;
@@ -395,7 +398,9 @@ static int coresident_direct_blocks(int device) {
       best = std::min(best, per_cu);
     }
   std::lock_guard<std::mutex> lk(mu);
-  return cache[device] = best * ncu;
+  cache[device] = {best * ncu, ncu};
+  if (ncu_out) *ncu_out = ncu;
+  return best * ncu;
 }
 
 // MCCS_DIRECT_BLOCKS: most workgroups per rank of a direct launch (default
@@ -502,9 +507,9 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   // per rank (the virtual node ran n = 4 / 8 fastest at 64 / 32 workgroups
   // per rank, i.e. one per CU in all; two per CU cost up to 1.5x), and never
   // more than can be resident at once (they spin on each other's counts).
-  const int cap = coresident_direct_blocks(c0->device);
   int ncu = 0;
-  if (rt().CuCount(&ncu, c0->device) != hipSuccess || ncu <= 0) ncu = cap;
+  const int cap = coresident_direct_blocks(c0->device, &ncu);
+  if (ncu <= 0) ncu = cap;
   // scatter bytes per workgroup (MCCS_DIRECT_WG_BYTES): 4 KiB beat 8 / 16 KiB
   // on the virtual node at 32-512 KiB (n = 8 32 KiB one-shot 19.1 -> 14.4 us,
   // 16 KiB: 27.0) and tied 2 KiB (pieces are >= 4 KiB)
