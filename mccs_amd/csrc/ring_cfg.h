@@ -125,7 +125,8 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 // totals of what it has been sent so far (E_IN, E_OUT) and waits for
 // total + this launch's share.  Launch seq s (1, 2, ...) and the totals are
 // advanced in the control block by the last workgroup of a launch to arrive
-// (after every workgroup read them), so graph replays keep counting.  Reuse across back-to-back launches:
+// (after every workgroup read them), so graph replays keep counting.
+// Reuse across back-to-back launches:
 //   two-shot slots: a rank's in slots are refilled (phase 1 of launch s+1,
 //     which waits for nothing) only by a peer that finished launch s, which
 //     needed this rank's broadcast of s (or this rank owned nothing and read
@@ -134,6 +135,10 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 //   one-shot slots alternate by parity s & 1: a peer writes parity p in
 //     launch s+2 only after finishing s+1, which needed this rank's writes of
 //     s+1, made after this rank finished reading parity p in launch s.
+// Both hold across any mix of variants (and AllGather): a peer cannot finish
+// a launch without a hand-off this rank makes in that same launch (with
+// count >= 1 some rank owns elements, and whoever it is waits, directly or
+// through its broadcast, for this rank's phase-1 count).
 #define MCCS_DIRECT_MAX_RANKS 8
 #define MCCS_DIRECT_CTRL_BYTES 65536
 // u64, added to by sender s; a rank's own line IN_CNT(rank) counts its own
