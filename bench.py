@@ -164,27 +164,52 @@ def host_loopback_latency(calls: int = 200) -> dict:
     """BASELINE configs[0]: 2-rank loopback AllReduce of 1 KiB fp32 on host
     threads (mccs_host_ring_allreduce: the ring protocol over host memory,
     reference schema 1 channel x 96 threads).  Median wall time per call over
-    `calls` calls; the result is checked against a + b (n = 2: exact)."""
+    `calls` calls, timed at the C ABI with the pointer arrays built once (as a
+    Rust caller holds its raw pointers), and through the Python wrapper
+    (which rebuilds them per call); every result is checked against a + b
+    (n = 2: exact)."""
     import numpy as np
 
+    from mccs_amd import _lib
     from mccs_amd import comm as C
 
     rng = np.random.default_rng(0x6D636373)
     send = [(rng.random(256, dtype=np.float32) * 2 - 1) for _ in range(2)]
-    recv = [np.empty_like(x) for x in send]
-    ts = []
-    for i in range(calls + 10):
-        t0 = time.perf_counter()
-        C.host_ring_allreduce(send, recv, 256, C.AllReduceDataType.Float32, channels=1, nthreads=96)
-        if i >= 10:
-            ts.append(time.perf_counter() - t0)
     exp = send[0] + send[1]
-    if not all(np.array_equal(r, exp) for r in recv):
-        raise SystemExit("configs[0] host loopback: result mismatch")
-    ts.sort()
+    fn = _lib.load().mccs_host_ring_allreduce
+    f32 = int(C.AllReduceDataType.Float32)
+
+    def timed(call):
+        recv = [np.empty_like(x) for x in send]
+        ts = []
+        for i in range(calls + 10):
+            for r in recv:
+                r.fill(np.nan)
+            t0 = time.perf_counter()
+            call(recv)
+            if i >= 10:
+                ts.append(time.perf_counter() - t0)
+            if not all(np.array_equal(r, exp) for r in recv):
+                raise SystemExit("configs[0] host loopback: result mismatch")
+        ts.sort()
+        return ts
+
+    sp = _lib.ptr_array([x.ctypes.data for x in send])
+    arrays = {}
+
+    def c_abi(recv):
+        rp = arrays.get(id(recv[0]))
+        if rp is None:
+            rp = arrays[id(recv[0])] = _lib.ptr_array([x.ctypes.data for x in recv])
+        _lib.check(fn(2, sp, rp, 256, f32, 0, 1, 96, 1 << 22, None), "mccs_host_ring_allreduce")
+
+    ts = timed(c_abi)
+    tw = timed(lambda recv: C.host_ring_allreduce(send, recv, 256, C.AllReduceDataType.Float32, channels=1,
+                                                  nthreads=96))
     return {"workload": "2-rank loopback allreduce, 1 KiB fp32, host-side sum (BASELINE configs[0])",
             "median_us": round(ts[len(ts) // 2] * 1e6, 2), "p10_us": round(ts[len(ts) // 10] * 1e6, 2),
-            "p90_us": round(ts[9 * len(ts) // 10] * 1e6, 2), "calls": calls, "exact": True}
+            "p90_us": round(ts[9 * len(ts) // 10] * 1e6, 2), "timed_at": "C ABI (ctypes call, pointer arrays built once)",
+            "python_wrapper_median_us": round(tw[len(tw) // 2] * 1e6, 2), "calls": calls, "exact": True}
 
 
 def load_pmc_traffic(tag: str):

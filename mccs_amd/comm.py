@@ -260,8 +260,9 @@ def host_ring_allreduce(sendbufs, recvbufs, count: int, data_type, op_type=AllRe
     """BASELINE configs[0]: the ring protocol on host threads over host memory
     (numpy arrays or raw host pointers; no GPU)."""
     n = len(sendbufs)
-    sp = _lib.ptr_array([x.ctypes.data if hasattr(x, "ctypes") else int(x) for x in sendbufs])
-    rp = _lib.ptr_array([x.ctypes.data if hasattr(x, "ctypes") else int(x) for x in recvbufs])
+    arr = ctypes.c_void_p * max(1, n)
+    sp = arr(*[x.ctypes.data if hasattr(x, "ctypes") else int(x) for x in sendbufs])
+    rp = arr(*[x.ctypes.data if hasattr(x, "ctypes") else int(x) for x in recvbufs])
     ro = None
     if rings is not None:
         flat = [int(v) for r in rings for v in r]

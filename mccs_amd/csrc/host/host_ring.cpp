@@ -145,7 +145,10 @@ struct HostConn {  // one directed FIFO (rank -> next) of one channel
   // uninitialised: only the slots a call touches are ever faulted in (a
   // zero-filled 4 MiB FIFO per connector cost ms per 1 KiB call)
   std::unique_ptr<char[]> data;
-  std::atomic<uint64_t> head{0}, tail{0};
+  // written by different threads (head: receiver, tail: sender): one cache
+  // line each, so a post does not invalidate the line the other side polls
+  alignas(64) std::atomic<uint64_t> head{0};
+  alignas(64) std::atomic<uint64_t> tail{0};
 };
 
 struct Ctx {
@@ -162,7 +165,7 @@ struct Ctx {
 // one (rank, channel) thread executing runRing
 void run_rank_channel(Ctx* c, int rank, int ch) {
   const int n = c->n;
-  std::vector<int> ring(n);
+  int ring[64];  // n <= 64 (mccs_host_ring_allreduce)
   for (int i = 0; i < n; ++i) ring[i] = c->rings ? c->rings[ch * n + i] : i;
   int pos = 0, pos0 = 0;
   for (int i = 0; i < n; ++i) {
@@ -227,10 +230,15 @@ void run_rank_channel(Ctx* c, int rank, int ch) {
         if (DST) std::memcpy(output + (dstIx + offset) * c->es, tmp, bytes);
         if (SEND) std::memcpy(sslot, tmp, bytes);
       }
-      if (SEND) out.tail.store(sstep + 2, std::memory_order_release);
-      if (RECV) in.head.store(rstep + 2, std::memory_order_release);
-      if (RECV) rstep += 2;
-      if (SEND) sstep += 2;
+      // a call whose elements all fit in this slice posts the steps of its
+      // remaining (empty) slices with this one: the same step counts as a
+      // post per slice, one cross-thread hand-off instead of two
+      const int64_t adv = offset + sliceSize >= nelem ? 2 * (2 - slice) : 2;
+      if (SEND) out.tail.store(sstep + adv, std::memory_order_release);
+      if (RECV) in.head.store(rstep + adv, std::memory_order_release);
+      if (RECV) rstep += adv;
+      if (SEND) sstep += adv;
+      if (adv > 2) break;
       offset += sliceSize;
     }
     return true;
@@ -261,7 +269,7 @@ void run_rank_channel(Ctx* c, int rank, int ch) {
 
 // Parked worker threads, one per concurrent (rank, channel) task: every task
 // of a call must run at the same time (they spin on each other's FIFO flags),
-// so task i always goes to worker i.  Workers spin briefly after a call (back
+// so task i >= 1 always goes to worker i and task 0 runs on the caller.  Workers spin briefly after a call (back
 // to back calls wake them in ~1 us) and then sleep on a condition variable.
 class HostRingPool {
  public:
@@ -285,19 +293,24 @@ class HostRingPool {
     return conns_;
   }
 
+  // Task 0 runs on the calling thread; tasks 1.. go to parked workers 1..
+  // (a 2-rank call wakes one worker).  The job is published through gen_
+  // (release) and picked up with an acquire load, so a spinning worker
+  // starts without touching the mutex.
   void run(Ctx* c, int ntasks) {
-    while ((int)workers_.size() < ntasks) {
-      const int id = (int)workers_.size();
+    while ((int)workers_.size() < ntasks - 1) {
+      const int id = (int)workers_.size() + 1;
       workers_.emplace_back([this, id] { loop(id); });
     }
-    remaining_.store(ntasks, std::memory_order_relaxed);
+    remaining_.store(ntasks - 1, std::memory_order_relaxed);
+    job_.store(c, std::memory_order_relaxed);
+    ntasks_.store(ntasks, std::memory_order_relaxed);
     {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = c;
-      ntasks_ = ntasks;
+      std::lock_guard<std::mutex> lk(mu_);  // pairs with a sleeper's predicate check
       gen_.fetch_add(1, std::memory_order_release);
     }
-    cv_.notify_all();
+    if (sleepers_.load(std::memory_order_acquire)) cv_.notify_all();
+    run_rank_channel(c, 0, 0);
     for (int spin = 0; remaining_.load(std::memory_order_acquire) != 0; ++spin) {
       if (spin < 4096) __builtin_ia32_pause();
       else std::this_thread::yield();
@@ -310,21 +323,19 @@ class HostRingPool {
     for (;;) {
       // spin ~200 us for the next call, then sleep
       const auto t0 = std::chrono::steady_clock::now();
-      while (gen_.load(std::memory_order_acquire) == seen &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+      for (int i = 0; gen_.load(std::memory_order_acquire) == seen; ++i) {
         __builtin_ia32_pause();
+        if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+      }
       if (gen_.load(std::memory_order_acquire) == seen) {
         std::unique_lock<std::mutex> lk(mu_);
+        sleepers_.fetch_add(1, std::memory_order_acq_rel);
         cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+        sleepers_.fetch_sub(1, std::memory_order_acq_rel);
       }
-      Ctx* c;
-      int ntasks;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        seen = gen_.load(std::memory_order_acquire);
-        c = job_;
-        ntasks = ntasks_;
-      }
+      seen = gen_.load(std::memory_order_acquire);
+      Ctx* c = job_.load(std::memory_order_relaxed);
+      const int ntasks = ntasks_.load(std::memory_order_relaxed);
       if (id < ntasks) {
         run_rank_channel(c, id / c->nch, id % c->nch);
         remaining_.fetch_sub(1, std::memory_order_acq_rel);
@@ -339,8 +350,9 @@ class HostRingPool {
   std::condition_variable cv_;
   std::atomic<uint64_t> gen_{0};
   std::atomic<int> remaining_{0};
-  Ctx* job_ = nullptr;
-  int ntasks_ = 0;
+  std::atomic<int> sleepers_{0};
+  std::atomic<Ctx*> job_{nullptr};
+  std::atomic<int> ntasks_{0};
 };
 
 }  // namespace
