@@ -144,6 +144,10 @@ typedef struct {
                            every chunk itself (same order, same bits; one exchange instead of
                            two).  0 = default (MCCS_ONESHOT_BYTES; else 2 MiB at 2 ranks, 1 MiB at
                            3-4, 256 KiB above), < 0 = never; ranks must agree */
+  int ll_bytes;         /* AllReduce buckets of at most this many bytes per rank take the LL one-shot
+                           (flag-carrying 16-byte lines: no drain, no count atomic) when the arena is
+                           uncached; same order, same bits.  0 = default (MCCS_LL_BYTES; else 128 KiB),
+                           < 0 = never, at most 1 MiB; ranks must agree (appended in 0.3.1) */
 } mccsCommConfig;
 
 void mccsCommConfigDefault(mccsCommConfig *cfg);
@@ -190,10 +194,11 @@ mccsResult_t mccsCommInfo(mccsComm_t comm, int *info7);
 /* ring send order of channel ch (nranks ints). */
 mccsResult_t mccsCommRing(mccsComm_t comm, int ch, int *order);
 /* Algorithm of the comm's latest launch: MCCS_ALGO_RING, MCCS_ALGO_DIRECT
- * (two-shot) or MCCS_ALGO_ONESHOT (-1 before the first). */
+ * (two-shot), MCCS_ALGO_ONESHOT or MCCS_ALGO_LL (LL one-shot) (-1 before the first). */
 #define MCCS_ALGO_RING 0
 #define MCCS_ALGO_DIRECT 1
 #define MCCS_ALGO_ONESHOT 2
+#define MCCS_ALGO_LL 3
 int mccsCommLastAlgo(mccsComm_t comm);
 /* 1 when the comm may run the direct kernel: a direct region was configured
  * and every device of the communicator can perform atomics on every other's
@@ -253,6 +258,8 @@ int mccs_default_rings(int nranks, int nch_req, int *out, int max_channels);
  * mccsCommConfig.oneshot_bytes / direct_bytes = 0 resolve to without the
  * MCCS_* overrides; -1 = off). */
 void mccs_direct_defaults(int nranks, int *oneshot_bytes, int *direct_bytes);
+/* mccsCommConfig.ll_bytes = 0 resolves to this (without the environment override). */
+int mccs_ll_default(int nranks);
 /* get_task_schema (plan.rs:602-635): channels and threads for total_bytes. */
 void mccs_task_schema(size_t total_bytes, int nch_cfg, int *nch, int *nthreads);
 

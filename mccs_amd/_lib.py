@@ -71,7 +71,7 @@ class _CommConfig(ctypes.Structure):
                 ("block_threads", _c_int), ("locality", _c_int), ("fifo_memory", _c_int),
                 ("timeout_ms", _c_int), ("work_fifo_depth", _c_int), ("bridge_streams", _c_int),
                 ("rings", _P(_c_int)), ("fifo_slots", _c_int), ("direct_bytes", _c_int),
-                ("oneshot_bytes", _c_int)]
+                ("oneshot_bytes", _c_int), ("ll_bytes", _c_int)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/mccs_hip.h
@@ -107,6 +107,7 @@ SIGNATURES: dict[str, tuple] = {
     "mccsCommRing": (_c_int, [_c_void_p, _c_int, _P(_c_int)]),
     "mccsCommDevComm": (_c_int, [_c_void_p, _P(_c_void_p)]),
     "mccsCommLastAlgo": (_c_int, [_c_void_p]),
+    "mccs_ll_default": (_c_int, [_c_int]),
     "mccsCommDirectEnabled": (_c_int, [_c_void_p]),
     "mccs_ring_profile": (_c_int, [_c_int, _P(ctypes.c_ulonglong), _c_int]),
     "mccsMemAllocShared": (_c_int, [_c_int, _c_size_t, _P(_c_void_p), _c_void_p]),

@@ -83,6 +83,7 @@ class CommConfig:
     fifo_slots: int | None = None  # FIFO slots per connection: 8 (reference), 16, 32
     direct_bytes: int | None = None  # largest bucket (bytes per rank) for the direct two-shot kernel; < 0 never
     oneshot_bytes: int | None = None  # largest bucket for the one-shot variant; < 0 never
+    ll_bytes: int | None = None  # largest bucket for the LL one-shot (uncached arenas); < 0 never
 
     def to_c(self, nranks: int):
         c = _CommConfig()
@@ -149,7 +150,7 @@ class Communicator:
         """"ring", "direct" (two-shot) or "oneshot": the algorithm of the latest
         launch (None before one)."""
         a = _sig().mccsCommLastAlgo(self._h)
-        return {0: "ring", 1: "direct", 2: "oneshot"}.get(a)
+        return {0: "ring", 1: "direct", 2: "oneshot", 3: "ll"}.get(a)
 
     def direct_enabled(self) -> bool:
         """Whether AllReduces may take the direct kernel (a direct region is
@@ -292,6 +293,11 @@ def direct_defaults(nranks: int) -> tuple[int, int]:
     return a.value, b.value
 
 
+def ll_default(nranks: int) -> int:
+    """ll_bytes the library uses by default for n ranks (-1 = off); host-only."""
+    return int(_sig().mccs_ll_default(int(nranks)))
+
+
 def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
     a, b = _ci(), _ci()
     _sig().mccs_task_schema(total_bytes, channels, ctypes.byref(a), ctypes.byref(b))
@@ -300,6 +306,6 @@ def task_schema(total_bytes: int, channels: int) -> tuple[int, int]:
 
 __all__ = ["AllReduceDataType", "AllReduceOpType", "CommConfig", "Communicator", "init_all",
            "init_communicator_rank", "all_reduce", "all_gather", "group", "default_rings", "task_schema",
-           "direct_defaults",
+           "direct_defaults", "ll_default",
            "host_ring_allreduce", "ring_profile",
            "RedOp", "DataType"]

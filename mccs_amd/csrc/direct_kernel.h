@@ -509,9 +509,181 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   MCCS_DTRACE(kDtEnd);
 }
 
+// ---- LL one-shot (ring_cfg.h): the smallest buckets, thread-linear over the
+// bucket's 8-byte words.  Word w belongs to global thread w mod (G x threads)
+// in both phases, so an in-place call overwrites a word only after the same
+// thread has read and sent it.  Each word's chunk (and so its ring order) is
+// found from the walk: chunk offsets are multiples of the realChunkSize
+// granule ((nthr_ref - 64) x 8 bytes), so no word straddles two chunks.
+template <typename T>
+__device__ __forceinline__ uint64_t ll_load_word(const char* base, uint32_t wd, uint32_t size, bool aligned) {
+  constexpr uint32_t EPW = 8 / sizeof(T);
+  const uint32_t e = wd * EPW;
+  if (aligned && e + EPW <= size) return __builtin_nontemporal_load((const uint64_t*)base + wd);
+  uint64_t v = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < EPW; ++j)
+    if (e + j < size) {
+      const T x = ((const T*)base)[e + j];
+      uint64_t b = 0;
+      __builtin_memcpy(&b, &x, sizeof(T));
+      v |= b << (8 * sizeof(T) * j);
+    }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void ll_store_word(char* base, uint32_t wd, uint32_t size, bool aligned, uint64_t v) {
+  constexpr uint32_t EPW = 8 / sizeof(T);
+  const uint32_t e = wd * EPW;
+  if (aligned && e + EPW <= size) {
+    __builtin_nontemporal_store(v, (uint64_t*)base + wd);
+    return;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < EPW; ++j)
+    if (e + j < size) {
+      const uint64_t b = v >> (8 * sizeof(T) * j);
+      T x;
+      __builtin_memcpy(&x, &b, sizeof(T));
+      ((T*)base)[e + j] = x;
+    }
+}
+
+__device__ __forceinline__ u32x4 ll_pack(uint64_t v) {
+  u32x4 p;
+  p.x = (uint32_t)v;
+  p.y = (uint32_t)(v >> 32);
+  p.z = 0;
+  p.w = 0;
+  return p;
+}
+
+template <int DT, int OP>
+__device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
+  using T = typename Elem<DT>::T;
+  constexpr uint32_t EPW = 8 / sizeof(T);
+  __shared__ uint64_t s_seq;
+  __shared__ int s_ok;
+  __shared__ uint8_t s_idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];
+  const mccsDirectRank& me = a.r[blockIdx.y];
+  const uint32_t n = a.nranks, rank = me.rank;
+  char* const mine = me.region[rank];
+  volatile uint32_t* abortFlag = me.abort_flag;
+  mccsRingKernelCfg ecfg{};
+  ecfg.err_line = me.err_line;
+  const DirectWalk w = direct_walk<DT>(a);
+  const uint32_t nwords = (uint32_t)(((uint64_t)w.size * sizeof(T) + 7) / 8);
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const char* in = (const char*)me.send;
+  char* out = (char*)me.recv;
+  const bool in_al = ((uintptr_t)in & 7) == 0, out_al = ((uintptr_t)out & 7) == 0;
+  // the first word's input load is in flight while thread 0 reads the launch
+  // count: the prologue costs one round trip
+  uint64_t own0 = 0;
+  if (gtid < nwords) own0 = ll_load_word<T>(in, gtid, w.size, in_al);
+  if (threadIdx.x == 0) {
+    s_seq = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_STATE) + MCCS_DIRECT_ST_LAUNCHES, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT) + 1;
+    s_ok = !abort_raised(abortFlag);
+  }
+  if (threadIdx.x < 64) ((uint32_t*)s_idx2rank)[threadIdx.x] = ((const uint32_t*)a.idx2rank)[threadIdx.x];
+  __syncthreads();
+  // every workgroup has read the launch count once it arrives; the last one
+  // to arrive advances it (after phase 1)
+  uint32_t arrived = 0;
+  if (threadIdx.x == 0)
+    arrived = __hip_atomic_fetch_add((uint32_t*)(mine + MCCS_DIRECT_DONE), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t seq = s_seq;
+  const uint64_t flag = (uint64_t)(uint32_t)seq << 32;
+  const int64_t lslot = (int64_t)a.ll_slot_bytes;
+  const int64_t llbase = MCCS_DIRECT_CTRL_BYTES + (int64_t)MCCS_DIRECT_SLOTS * (int64_t)a.slot_bytes +
+                         2 * (int64_t)MCCS_DIRECT_MAX_RANKS * (int64_t)a.oslot_bytes +
+                         (int64_t)(seq & 1) * MCCS_DIRECT_MAX_RANKS * lslot;
+  bool ok = s_ok != 0;
+  // 1. every word to every peer's LL slot, as a flag-carrying line
+  if (ok)
+    for (uint32_t wd = gtid; wd < nwords; wd += stride) {
+      const uint64_t v = wd == gtid ? own0 : ll_load_word<T>(in, wd, w.size, in_al);
+      const uint64_t lo = flag | (v & 0xffffffffull), hi = flag | (v >> 32);
+#pragma unroll
+      for (uint32_t t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
+        if (t < n && t != rank) {
+          uint64_t* p = (uint64_t*)(me.region[t] + llbase + (int64_t)rank * lslot + (int64_t)wd * 16);
+          __hip_atomic_store(p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+  if (threadIdx.x == 0 && arrived + 1 == gridDim.x) {
+    __hip_atomic_store((uint32_t*)(mine + MCCS_DIRECT_DONE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((uint64_t*)(mine + MCCS_DIRECT_STATE) + MCCS_DIRECT_ST_LAUNCHES, seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 2. poll every peer's line of each word, reduce in the ring's order
+  const uint32_t peers = ((1u << n) - 1u) & ~(1u << rank);
+  const uint32_t seq32 = (uint32_t)seq;
+  const uint32_t parts = w.nch * n;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t wd = gtid; ok && wd < nwords; wd += stride) {
+    const uint32_t e = wd * EPW;
+    const uint32_t g = e / w.loopSize * w.loopSize;
+    uint32_t rcs = (w.size - g + parts - 1) / parts;  // realChunkSize, all_reduce.h:30-36
+    rcs = w.chunkSize < rcs ? w.chunkSize : rcs;
+    rcs = (rcs + w.gran - 1) / w.gran * w.gran;
+    const uint32_t c = (e - g) / rcs, bid = c / n, k = c - bid * n;
+    const uint64_t own = wd == gtid ? own0 : ll_load_word<T>(in, wd, w.size, in_al);
+    const char* lb = mine + llbase + (int64_t)wd * 16;
+    uint64_t h0[MCCS_DIRECT_MAX_RANKS], h1[MCCS_DIRECT_MAX_RANKS];
+    uint32_t pending = peers, spins = 0;
+    for (;;) {
+#pragma unroll
+      for (uint32_t t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
+        if ((pending >> t) & 1u) {
+          const uint64_t* p = (const uint64_t*)(lb + (int64_t)t * lslot);
+          h0[t] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          h1[t] = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+#pragma unroll
+      for (uint32_t t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
+        if (((pending >> t) & 1u) && (uint32_t)(h0[t] >> 32) == seq32 && (uint32_t)(h1[t] >> 32) == seq32)
+          pending &= ~(1u << t);
+      if (!pending) break;
+      if (++spins % 64 == 0) {
+        const bool ab = abort_raised(abortFlag);
+        const bool to = !ab && a.timeout_ticks && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
+        if (ab || to) {
+          raise_error(abortFlag, ecfg, ab ? MCCS_ERR_ABORTED : MCCS_ERR_TIMEOUT);
+          ok = false;
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(MCCS_POLL_SLEEP);
+    }
+    if (!ok) break;
+    // acc = x[idx k+1]; acc = fn(x[idx k+j], acc)
+    u32x4 acc{};
+#pragma unroll
+    for (uint32_t j = 0; j < MCCS_DIRECT_MAX_RANKS; ++j)
+      if (j < n) {
+        uint32_t idx = k + 1 + j;
+        idx = idx >= n ? idx - n : idx;
+        const uint32_t q = s_idx2rank[bid][idx];
+        uint64_t v = own;
+#pragma unroll
+        for (uint32_t t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
+          if (t == q && t != rank) v = (h0[t] & 0xffffffffull) | (h1[t] << 32);
+        acc = j == 0 ? ll_pack(v) : pack_op<DT, OP>(ll_pack(v), acc);
+      }
+    ll_store_word<T>(out, wd, w.size, out_al, (uint64_t)acc.x | ((uint64_t)acc.y << 32));
+  }
+}
+
 template <int DT, int OP>
 __global__ void __launch_bounds__(MCCS_DIRECT_THREADS) direct_kernel(mccsDirectArgs a) {
-  direct_body<DT, OP>(a);
+  if (a.mode == MCCS_DIRECT_LL_ONE_SHOT) direct_ll_body<DT, OP>(a);
+  else direct_body<DT, OP>(a);
 }
 
 }  // namespace mccs

@@ -45,6 +45,18 @@ static int default_oneshot_bytes(int nranks) {
   return nranks == 2 ? 2 << 20 : nranks <= 4 ? 1 << 20 : 256 << 10;
 }
 static int default_direct_bytes(int nranks) { return nranks >= 4 ? 8 << 20 : nranks == 3 ? 4 << 20 : -1; }
+// LL one-shot (ring_cfg.h): buckets whose hand-off round trips cost more than
+// their bytes; its lines carry 8 data bytes per 16, so it stays small.
+// Virtual node, graph replay, fp16 (profiles/r03_direct_ll_vnode.json): LL
+// beat the one-shot at every n up to 128 KiB (n = 8: 32 KiB 15.1 -> 8.6 us,
+// 128 KiB 22.0 -> 14.2; n = 2: 32 KiB 8.4 -> 5.0) and lost at n = 8 from
+// 512 KiB.  Over xGMI its doubled line bytes cost link time
+// (2 x 128 KiB per peer link ~ 4 us at ~64 GB/s, about the round trips it
+// saves), so the default stays at 128 KiB for every n.
+static int default_ll_bytes(int nranks) {
+  (void)nranks;
+  return 128 << 10;
+}
 
 static void fill_defaults(mccsCommConfig* c, int nranks) {
   if (c->buffer_size <= 0) c->buffer_size = 1 << 22;  // mccs.toml:19
@@ -61,6 +73,7 @@ static void fill_defaults(mccsCommConfig* c, int nranks) {
   if (c->fifo_slots == 0) c->fifo_slots = 2 * MCCS_BUFFER_SLOTS;
   if (c->direct_bytes == 0) c->direct_bytes = default_direct_bytes(nranks);
   if (c->oneshot_bytes == 0) c->oneshot_bytes = default_oneshot_bytes(nranks);
+  if (c->ll_bytes == 0) c->ll_bytes = default_ll_bytes(nranks);
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
@@ -82,6 +95,7 @@ static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
   if (c.fifo_slots != 8 && c.fifo_slots != 16 && c.fifo_slots != 32) return mccsInvalidArgument;
   if (c.direct_bytes > (1 << 30)) return mccsInvalidArgument;    // 9 slots of it live in every rank's arena
   if (c.oneshot_bytes > (64 << 20)) return mccsInvalidArgument;  // 16 slots of it
+  if (c.ll_bytes > (1 << 20)) return mccsInvalidArgument;        // 16 slots of twice it
   return mccsSuccess;
 }
 
@@ -215,6 +229,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   if (const char* v = std::getenv("MCCS_FIFO_SLOTS")) cfg->fifo_slots = std::atoi(v);
   if (const char* v = std::getenv("MCCS_DIRECT_BYTES")) cfg->direct_bytes = std::atoi(v);
   if (const char* v = std::getenv("MCCS_ONESHOT_BYTES")) cfg->oneshot_bytes = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_LL_BYTES")) cfg->ll_bytes = std::atoi(v);
 }
 
 extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {
@@ -476,7 +491,7 @@ extern "C" int mccsCommLastAlgo(mccsComm_t comm) {
 
 extern "C" int mccsCommDirectEnabled(mccsComm_t comm) {
   const Comm* c = (const Comm*)comm;
-  return c && c->direct_ok && (c->layout.direct_slot > 0 || c->layout.oneshot_slot > 0);
+  return c && c->direct_ok && (c->layout.direct_slot > 0 || c->layout.oneshot_slot > 0 || c->layout.ll_slot > 0);
 }
 
 extern "C" mccsResult_t mccsCommDevComm(mccsComm_t comm, void** dev_comm) {
@@ -510,6 +525,8 @@ extern "C" int mccs_default_rings(int nranks, int nch_req, int* out, int max_cha
     for (int i = 0; i < nranks; ++i) out[c * nranks + i] = rings[c][i];
   return n;
 }
+
+extern "C" int mccs_ll_default(int nranks) { return default_ll_bytes(nranks); }
 
 extern "C" void mccs_direct_defaults(int nranks, int* oneshot_bytes, int* direct_bytes) {
   if (oneshot_bytes) *oneshot_bytes = default_oneshot_bytes(nranks);

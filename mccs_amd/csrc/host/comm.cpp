@@ -212,6 +212,9 @@ mccsResult_t comm_alloc_local(Comm* c) {
       direct_ok && c->cfg.direct_bytes > 0 ? ((size_t)c->cfg.direct_bytes + 65535) & ~(size_t)65535 : 0;
   c->layout.oneshot_slot =
       direct_ok && c->cfg.oneshot_bytes > 0 ? ((size_t)c->cfg.oneshot_bytes + 65535) & ~(size_t)65535 : 0;
+  // exactly 2 x ll_bytes (8-byte multiple): ranks that disagree on ll_bytes
+  // get different arena sizes, which Connect refuses
+  c->layout.ll_slot = direct_ok && c->cfg.ll_bytes > 0 ? 2 * (((size_t)c->cfg.ll_bytes + 7) & ~(size_t)7) : 0;
   const size_t bytes = c->layout.total();
   c->own_arena = nullptr;
   c->own_arena_uncached = false;

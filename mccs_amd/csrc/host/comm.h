@@ -60,7 +60,7 @@ struct DeviceGuard {
 // Per-rank FIFO arena layout (identical on every rank; offsets in bytes).
 // [flags: nch x {send head lines, recv tail lines}] [data: nch x fifo_bytes]
 // [direct region (64 KiB aligned), when direct_slot or oneshot_slot > 0:
-//  control + the slots of the direct AllReduce, ring_cfg.h]
+//  control + the slots of the direct AllReduce (two-shot, one-shot, LL), ring_cfg.h]
 // fifo_bytes = fifo_slots x buffer_size / 8 (slots of the reference step size)
 struct ArenaLayout {
   int nch = 0;
@@ -68,6 +68,7 @@ struct ArenaLayout {
   size_t fifo_bytes = 0;
   size_t direct_slot = 0;   // bytes of one two-shot in/out slot
   size_t oneshot_slot = 0;  // bytes of one one-shot slot
+  size_t ll_slot = 0;       // bytes of one LL one-shot slot (2 x the LL bucket bytes)
   static constexpr size_t kLinesBytes = (size_t)MCCS_MAX_LANES * MCCS_FLAG_LINE_BYTES;  // 8 KiB
   size_t head_off(int c) const { return (size_t)c * 2 * kLinesBytes; }
   size_t tail_off(int c) const { return (size_t)c * 2 * kLinesBytes + kLinesBytes; }
@@ -76,9 +77,10 @@ struct ArenaLayout {
   size_t ring_total() const { return flags_bytes() + (size_t)nch * fifo_bytes; }
   size_t direct_off() const { return (ring_total() + 65535) & ~(size_t)65535; }
   size_t total() const {
-    return direct_slot || oneshot_slot ? direct_off() + MCCS_DIRECT_CTRL_BYTES + (size_t)MCCS_DIRECT_SLOTS * direct_slot +
-                                             2 * (size_t)MCCS_DIRECT_MAX_RANKS * oneshot_slot
-                                       : ring_total();
+    return direct_slot || oneshot_slot || ll_slot
+               ? direct_off() + MCCS_DIRECT_CTRL_BYTES + (size_t)MCCS_DIRECT_SLOTS * direct_slot +
+                     2 * (size_t)MCCS_DIRECT_MAX_RANKS * (oneshot_slot + ll_slot)
+               : ring_total();
   }
 };
 

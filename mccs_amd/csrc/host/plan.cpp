@@ -110,6 +110,13 @@ static mccsResult_t demote_direct(Comm* c) {
   return ring_enqueue(c, c->plan_func, c->plan_dtype, c->plan_op, c->direct.send, c->direct.recv, c->direct.count);
 }
 
+// The LL one-shot needs an uncached arena: its lines are polled with
+// system-scope loads, which a cached (device) arena's L2 could serve stale.
+static bool ll_fits(const Comm* c, size_t bytes) {
+  return c->layout.ll_slot > 0 && c->own_arena_uncached && c->kcfg.fence_mode != MCCS_FENCE_SYSTEM &&
+         bytes <= (size_t)c->cfg.ll_bytes && 2 * ((bytes + 7) & ~(size_t)7) <= c->layout.ll_slot;
+}
+
 mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count) {
   if (c->plan_pending && (c->plan_func != func || c->plan_dtype != dtype || c->plan_op != op))
     return mccsInvalidUsage;  // pre_launch_schedule batches same func/dtype/op only (plan.rs:122-141)
@@ -122,8 +129,9 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   const size_t bytes = func == mccsFuncAllGather ? count : count * (size_t)elem_bytes(dtype);
   const bool oneshot = c->layout.oneshot_slot > 0 && bytes <= (size_t)c->cfg.oneshot_bytes;
   const bool twoshot = func == mccsFuncAllReduce && c->layout.direct_slot > 0 && bytes <= (size_t)c->cfg.direct_bytes;
+  const bool ll = func == mccsFuncAllReduce && ll_fits(c, bytes);
   if (!c->plan_pending && (func == mccsFuncAllReduce || func == mccsFuncAllGather) && c->direct_ok &&
-      (oneshot || twoshot)) {
+      (oneshot || twoshot || ll)) {
     c->plan_direct = true;
     c->direct.send = send;
     c->direct.recv = recv;
@@ -422,6 +430,7 @@ static bool direct_group(std::vector<Comm*>& comms, const std::vector<int>& idx)
         ck->plan_dtype != c0->plan_dtype ||
         ck->plan_op != c0->plan_op || ck->rings != c0->rings || ck->cfg.buffer_size != c0->cfg.buffer_size ||
         ck->layout.direct_slot != c0->layout.direct_slot || ck->layout.oneshot_slot != c0->layout.oneshot_slot ||
+        ck->layout.ll_slot != c0->layout.ll_slot || ck->cfg.ll_bytes != c0->cfg.ll_bytes ||
         ck->cfg.oneshot_bytes != c0->cfg.oneshot_bytes || ck->cfg.direct_bytes != c0->cfg.direct_bytes ||
         ck->nch != c0->nch)
       return false;
@@ -446,9 +455,15 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   da->count = c0->direct.count;
   da->slot_bytes = c0->layout.direct_slot;
   da->oslot_bytes = c0->layout.oneshot_slot;
+  da->ll_slot_bytes = c0->layout.ll_slot;
   const size_t nbytes = (size_t)c0->direct.count * esize;
-  const bool oneshot = c0->layout.oneshot_slot > 0 && nbytes <= (size_t)c0->cfg.oneshot_bytes;
-  da->mode = gather ? MCCS_DIRECT_AG_ONE_SHOT : oneshot ? MCCS_DIRECT_ONE_SHOT : MCCS_DIRECT_TWO_SHOT;
+  bool ll = !gather;  // every rank slot of the launch must take it (uncached arena)
+  for (size_t k = 0; k < idx.size(); ++k) ll = ll && ll_fits(comms[idx[k]], nbytes);
+  const bool oneshot = ll || (c0->layout.oneshot_slot > 0 && nbytes <= (size_t)c0->cfg.oneshot_bytes);
+  da->mode = gather ? MCCS_DIRECT_AG_ONE_SHOT
+             : ll   ? MCCS_DIRECT_LL_ONE_SHOT
+             : oneshot ? MCCS_DIRECT_ONE_SHOT
+                       : MCCS_DIRECT_TWO_SHOT;
   da->nranks = (uint32_t)n;
   da->nch = (uint32_t)chans.size();
   da->nthr_ref = (uint32_t)nthr;
@@ -519,6 +534,8 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
     return x >= 1024 ? x : 4096L;
   }();
   long g = std::min<long>((long)((scatter + wg_bytes - 1) / wg_bytes), direct_max_blocks());
+  // LL: one 8-byte word per thread
+  if (ll) g = std::min<long>((long)((nbytes + 8 * MCCS_DIRECT_THREADS - 1) / (8 * MCCS_DIRECT_THREADS)), direct_max_blocks());
   if (idx.size() > 1) g = std::min<long>(g, std::min(cap, ncu) / (long)idx.size());  // one fused launch
   else if (c0->share > 1) g = std::min<long>(g, std::min(cap / 2, ncu) / c0->share);  // separate processes
   g = std::max<long>(g, 1);
@@ -673,6 +690,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       comms[idx[k]]->event_recorded = record;
       comms[idx[k]]->last_algo = !direct                            ? MCCS_ALGO_RING
                                  : da.mode == MCCS_DIRECT_TWO_SHOT ? MCCS_ALGO_DIRECT
+                                 : da.mode == MCCS_DIRECT_LL_ONE_SHOT ? MCCS_ALGO_LL
                                                                    : MCCS_ALGO_ONESHOT;
     }
     c0->event_recorded = record || stop_on_launch;

@@ -240,7 +240,9 @@ class FakeRuntime final : public DeviceRuntime {
                 " nthr=" + std::to_string(da->nthr_ref) + " fence=" + std::to_string(da->fence_mode) +
                 " mode=" + (da->mode == MCCS_DIRECT_ONE_SHOT      ? "oneshot"
                             : da->mode == MCCS_DIRECT_AG_ONE_SHOT ? "ag-oneshot"
+                            : da->mode == MCCS_DIRECT_LL_ONE_SHOT ? "ll"
                                                                   : "twoshot") +
+                " gx=" + std::to_string(grid.x) + " llslot=" + std::to_string(da->ll_slot_bytes) +
                 " piece=" + std::to_string(da->piece) + " piece2=" + std::to_string(da->piece2) + " owned=";
         for (unsigned t = 0; t < da->nranks && t < MCCS_DIRECT_MAX_RANKS; ++t)
           extra += (t ? "," : "") + std::to_string(da->owned[t]);

@@ -118,6 +118,14 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 //   [two-shot in : MCCS_DIRECT_MAX_RANKS senders x slot_bytes]  (by element offset)
 //   [two-shot out: slot_bytes]
 //   [one-shot in : 2 parities x MCCS_DIRECT_MAX_RANKS senders x oslot_bytes]
+//   [LL one-shot : 2 parities x MCCS_DIRECT_MAX_RANKS senders x ll_slot_bytes]
+// LL one-shot (the smallest buckets): every 8 data bytes travel as one
+// 16-byte line {data lo, flag, data hi, flag} written with two 8-byte
+// system-scope stores, flag = the launch seq; a receiver polls the lines
+// themselves, so the hand-off needs no drain, no count atomic and no
+// separate flag round trip.  Its region is written only with such lines
+// (zero at init), so a line left from an earlier launch carries a smaller
+// seq; its slots alternate by parity like the one-shot's (same argument).
 // Hand-offs are element counts: a sender adds the elements it wrote into a
 // rank's slot to that rank's IN_CNT line (one remote atomic per workgroup and
 // target, after its stores drained), an owner adds the elements it broadcast
@@ -160,6 +168,7 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 #define MCCS_DIRECT_TWO_SHOT 0
 #define MCCS_DIRECT_ONE_SHOT 1
 #define MCCS_DIRECT_AG_ONE_SHOT 2  // AllGather: count = bytes per rank (dtype int8)
+#define MCCS_DIRECT_LL_ONE_SHOT 3  // one-shot through flag-carrying 16-byte lines (uncached arenas)
 
 struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
   const void* send;
@@ -175,6 +184,7 @@ struct mccsDirectArgs {
   uint64_t count;          // elements
   uint64_t slot_bytes;     // bytes of one two-shot slot (>= count * element size for two-shot)
   uint64_t oslot_bytes;    // bytes of one one-shot slot (>= count * element size for one-shot)
+  uint64_t ll_slot_bytes;  // bytes of one LL slot (>= 2 x count * element size, rounded to 8 bytes, for LL)
   uint64_t timeout_ticks;  // s_memrealtime ticks; 0 = never
   uint32_t nranks, nch, nthr_ref, buff_size;  // the ring walk this launch reproduces
   uint32_t fence_mode;                        // MCCS_FENCE_*

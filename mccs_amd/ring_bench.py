@@ -136,7 +136,7 @@ def _candidates(C, lanes_opts, locs, chan_opts=(None,)):
                 # fails over this node's links is caught by the watchdog within 20 s
                 # the ring at every size (the library's one-shot default would take
                 # the sweep's small buckets; direct_sweep times those variants)
-                kw = dict(locality=loc, lanes=lanes, timeout_ms=20000, direct_bytes=-1, oneshot_bytes=-1)
+                kw = dict(locality=loc, lanes=lanes, timeout_ms=20000, direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1)
                 if nch:
                     kw["channel_count"] = nch
                 tag = f"{lname}/lanes={lanes or 'auto'}" + (f"/channels={nch}" if nch else "")
@@ -395,8 +395,9 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
     ring = {r["bytes"]: r for r in ring_rows}
     comms, dead = {}, {}
     code = C.AllReduceDataType.Float16
-    for algo, kw in (("direct", dict(direct_bytes=upto, oneshot_bytes=-1)),
-                     ("oneshot", dict(direct_bytes=-1, oneshot_bytes=oneshot_upto))):
+    for algo, kw in (("direct", dict(direct_bytes=upto, oneshot_bytes=-1, ll_bytes=-1)),
+                     ("oneshot", dict(direct_bytes=-1, oneshot_bytes=oneshot_upto, ll_bytes=-1)),
+                     ("ll", dict(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=1 << 20))):
         cfg = dataclasses.replace(config or C.CommConfig(), **kw)
         try:
             comms[algo] = C.init_communicator_rank(rank, world, device, exchange, cfg)
@@ -417,7 +418,7 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
             if "graph_latency_us" in ring[nb]:
                 row["ring_graph_us"] = ring[nb]["graph_latency_us"]
         for algo, cm in comms.items():
-            if algo in dead or (algo == "oneshot" and nb > oneshot_upto):
+            if algo in dead or (algo == "oneshot" and nb > oneshot_upto) or (algo == "ll" and nb > 1 << 20):
                 continue
             el = gl = None
             err = None
@@ -461,16 +462,17 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
         out["rows"].append(row)
         del x, y
     best = {}
-    for algo in ("direct", "oneshot"):
+    for algo in ("direct", "oneshot", "ll"):
         wins = [r["bytes"] for r in out["rows"] if f"{algo}_graph_us" in r and "ring_graph_us" in r
                 and r[f"{algo}_graph_us"] < r["ring_graph_us"]]
         best[f"{algo}_beats_ring_upto_bytes"] = max(wins) if wins else 0
     # what the library's defaults pick at each size (thresholds of api.cpp)
     os_b, d_b = C.direct_defaults(world)
-    best["default_thresholds"] = {"oneshot_bytes": os_b, "direct_bytes": d_b}
+    ll_b = C.ll_default(world)
+    best["default_thresholds"] = {"ll_bytes": ll_b, "oneshot_bytes": os_b, "direct_bytes": d_b}
     for r in out["rows"]:
         nb = r["bytes"]
-        pick = ("oneshot" if 0 < nb <= os_b else "direct" if 0 < nb <= d_b else "ring")
+        pick = ("ll" if 0 < nb <= ll_b else "oneshot" if 0 < nb <= os_b else "direct" if 0 < nb <= d_b else "ring")
         if not out["p2p_atomics"] or f"{pick}_graph_us" not in r and pick != "ring":
             pick = "ring"
         r["default_algo"] = pick
@@ -794,7 +796,7 @@ def mode_config(C, mode: str, info: dict):
     fifo = {"uncached-fifo": C.FIFO_UNCACHED, "uncached-fifo+release-fence": C.FIFO_UNCACHED_RELEASE,
             "cached-fifo+system-fences": C.FIFO_DEVICE}.get(kind, C.FIFO_UNCACHED)
     return C.CommConfig(channel_count=info.get("channels"), lanes=info.get("lanes"), locality=loc, fifo_memory=fifo,
-                        timeout_ms=20000, direct_bytes=-1, oneshot_bytes=-1)
+                        timeout_ms=20000, direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1)
 
 
 def node_legs(torch, C, world, ndev, nbytes, config=None):

@@ -39,6 +39,7 @@ def _ring_unless_direct(request, monkeypatch):
     if not getattr(request.module, "DIRECT_DEFAULTS", False):
         monkeypatch.setenv("MCCS_ONESHOT_BYTES", "-1")
         monkeypatch.setenv("MCCS_DIRECT_BYTES", "-1")
+        monkeypatch.setenv("MCCS_LL_BYTES", "-1")
 
 
 @pytest.fixture(scope="session")

@@ -50,9 +50,12 @@ def main():
                  "sender-release": (C.FIFO_UNCACHED_RELEASE, C.LOCALITY_SENDER),
                  # the direct kernel (two-shot / one-shot) over IPC-mapped arenas
                  "direct": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
-                 "oneshot": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
-    direct_kw = {"direct": dict(direct_bytes=8 << 20, oneshot_bytes=-1),
-                 "oneshot": dict(direct_bytes=-1, oneshot_bytes=8 << 20)}
+                 "oneshot": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
+                 # LL one-shot up to 1 MiB (larger buckets: the one-shot)
+                 "ll": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
+    direct_kw = {"direct": dict(direct_bytes=8 << 20, oneshot_bytes=-1, ll_bytes=-1),
+                 "oneshot": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=-1),
+                 "ll": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=1 << 20)}
     names = os.environ.get("IPC_MODES", "uncached,device").split(",")
     results = {}
     # processes sharing one GPU: the library's default lanes; mccsCommConnect
@@ -92,7 +95,8 @@ def main():
                 print(f"[rank {rank}] {mode} code={code}: {e}", flush=True)
                 ok = False
             if mode in direct_kw:  # the call really took that kernel
-                ok = ok and comm.last_algo() == mode
+                want = "oneshot" if mode == "ll" and count * vnode.ESIZE[code] > 1 << 20 else mode
+                ok = ok and comm.last_algo() == want
             results[f"{mode}/dtype{code}/n{count}"] = ok
         if mode in direct_kw:  # several launches back to back, fresh inputs each, then one sync
             k = 12

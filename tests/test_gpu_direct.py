@@ -21,12 +21,16 @@ DIRECT_DEFAULTS = True  # conftest: keep the library's direct thresholds
 
 F16, F32, BF16, I32, F64, I8 = 6, 7, 9, 2, 8, 0
 DIRECT = 8 << 20
-VARIANTS = ["direct", "oneshot"]
+LL_MAX = 1 << 20  # the largest ll_bytes a comm accepts
+VARIANTS = ["direct", "oneshot", "ll"]
 
 
 def _cfg(variant="direct", **kw):
+    """One variant per comm.  "ll": the LL one-shot up to LL_MAX, larger
+    buckets the one-shot (so every test size has a direct kernel)."""
     kw.setdefault("direct_bytes", DIRECT if variant == "direct" else -1)
-    kw.setdefault("oneshot_bytes", DIRECT if variant == "oneshot" else -1)
+    kw.setdefault("oneshot_bytes", DIRECT if variant in ("oneshot", "ll") else -1)
+    kw.setdefault("ll_bytes", LL_MAX if variant == "ll" else -1)
     return C.CommConfig(**kw)
 
 
@@ -35,7 +39,9 @@ def _check(outs, exp):
         assert np.array_equal(o.view(np.uint8), exp.view(np.uint8)), f"rank {r} differs from oracle"
 
 
-def _algo(comms, want="direct"):
+def _algo(comms, want="direct", nbytes=None):
+    if want == "ll" and nbytes is not None and nbytes > LL_MAX:
+        want = "oneshot"
     assert all(c.last_algo() == want for c in comms), [c.last_algo() for c in comms]
 
 
@@ -48,7 +54,7 @@ def test_direct_matches_oracle(orc, n, code, variant):
         rng = np.random.default_rng(n * 10 + code)
         inputs = [vnode.gen(code, 300007, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, code, 0)
-        _algo(comms, variant)
+        _algo(comms, variant, inputs[0].nbytes)
         _check(outs, vnode.expected_allreduce(orc, inputs, code, 0, comms[0]))
     finally:
         vnode.destroy(comms)
@@ -64,7 +70,7 @@ def test_direct_every_dtype_and_op(orc, code, op, variant):
         rng = np.random.default_rng(code * 4 + op)
         inputs = [vnode.gen(code, 40013, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, code, op)
-        _algo(comms, variant)
+        _algo(comms, variant, inputs[0].nbytes)
         _check(outs, vnode.expected_allreduce(orc, inputs, code, op, comms[0]))
     finally:
         vnode.destroy(comms)
@@ -81,7 +87,7 @@ def test_direct_sizes(orc, count, variant):
         rng = np.random.default_rng(count)
         inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, F32, 0)
-        _algo(comms, variant)
+        _algo(comms, variant, inputs[0].nbytes)
         _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
@@ -100,7 +106,7 @@ def test_direct_multi_loop_walk(orc, n, variant):
         count = 3 * comms[0].nchannels * n * (buff // 8 // 2 * 4 // 2) + 12345
         inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, F16, 0)
-        _algo(comms, variant)
+        _algo(comms, variant, inputs[0].nbytes)
         _check(outs, vnode.expected_allreduce(orc, inputs, F16, 0, comms[0], buff_size=buff))
     finally:
         vnode.destroy(comms)
@@ -117,7 +123,7 @@ def test_direct_doubled_channels_and_custom_rings(orc, variant):
         rng = np.random.default_rng(5)
         inputs = [vnode.gen(BF16, 777777, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, BF16, 0)
-        _algo(comms, variant)
+        _algo(comms, variant, inputs[0].nbytes)
         _check(outs, vnode.expected_allreduce(orc, inputs, BF16, 0, comms[0]))
     finally:
         vnode.destroy(comms)
@@ -131,7 +137,7 @@ def test_direct_in_place(orc, variant):
         rng = np.random.default_rng(11)
         inputs = [vnode.gen(F32, 500001, rng) for _ in range(n)]
         outs = vnode.run_allreduce(comms, inputs, F32, 0, inplace=True)
-        _algo(comms, variant)
+        _algo(comms, variant, inputs[0].nbytes)
         _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
@@ -142,14 +148,15 @@ def test_direct_and_ring_interleaved(orc):
     the direct launches' running counts, the one-shot parity and the ring's
     FIFO steps all stay in lock-step, every result exact."""
     n = 4
-    comms = C.init_all([0] * n, C.CommConfig(direct_bytes=1 << 20, oneshot_bytes=64 << 10))
+    comms = C.init_all([0] * n, C.CommConfig(direct_bytes=1 << 20, oneshot_bytes=64 << 10, ll_bytes=16 << 10))
     try:
         rng = np.random.default_rng(3)
         for it, count in enumerate([1000, 300000, 262144, 16384, 16385, 262145, 5, 1 << 20, 77777, 3, 4] * 2):
             inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
             outs = vnode.run_allreduce(comms, inputs, F32, 0)
             nb = count * 4
-            _algo(comms, "oneshot" if nb <= 64 << 10 else "direct" if nb <= (1 << 20) else "ring")
+            _algo(comms, "ll" if nb <= 16 << 10 else "oneshot" if nb <= 64 << 10 else "direct" if nb <= (1 << 20)
+                  else "ring")
             _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
@@ -304,21 +311,22 @@ def test_direct_hand_off_modes(orc, fifo, variant):
         for count in (70001, 1 << 20):
             inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
             outs = vnode.run_allreduce(comms, inputs, F32, 0)
-            _algo(comms, variant)
+            # a cached arena never takes the LL one-shot
+            _algo(comms, "oneshot" if variant == "ll" and fifo == C.FIFO_DEVICE else variant, inputs[0].nbytes)
             _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
 
 
 def test_library_defaults(orc):
-    """The library defaults at n = 4: one-shot up to 1 MiB per rank, two-shot
-    up to 8 MiB, the ring above."""
+    """The library defaults at n = 4: LL one-shot up to 128 KiB per rank,
+    one-shot up to 1 MiB, two-shot up to 8 MiB, the ring above."""
     n = 4
     comms = C.init_all([0] * n)
     try:
         assert all(c.direct_enabled() for c in comms)
         rng = np.random.default_rng(44)
-        for count, want in ((1000, "oneshot"), (262144, "oneshot"), (262145, "direct"), (2 << 20, "direct"),
+        for count, want in ((1000, "ll"), (32768, "ll"), (32769, "oneshot"), (262144, "oneshot"), (262145, "direct"), (2 << 20, "direct"),
                             ((2 << 20) + 1, "ring")):
             inputs = [vnode.gen(F32, count, rng) for _ in range(n)]
             outs = vnode.run_allreduce(comms, inputs, F32, 0)
@@ -374,13 +382,13 @@ def test_allgather_oneshot(n, nbytes, inplace):
 
 def test_allgather_oneshot_back_to_back_and_mixed(orc):
     """AllGathers (one-shot and, above the threshold, ring) and AllReduces
-    (one-shot, two-shot) alternate without syncs in between; every output
+    (LL one-shot, one-shot, two-shot) alternate without syncs in between; every output
     exact (the one-shot slots' parity and the running counts are shared by
     both collectives)."""
     import torch
 
     n = 4
-    comms = C.init_all([0] * n, C.CommConfig(direct_bytes=1 << 20, oneshot_bytes=64 << 10))
+    comms = C.init_all([0] * n, C.CommConfig(direct_bytes=1 << 20, oneshot_bytes=64 << 10, ll_bytes=8 << 10))
     try:
         rng = np.random.default_rng(77)
         plan = [("ag", 5000), ("ar", 3000), ("ag", 70000), ("ar", 100000), ("ag", 65536), ("ar", 7), ("ag", 1)] * 3
@@ -413,7 +421,8 @@ def test_allgather_oneshot_back_to_back_and_mixed(orc):
                     assert np.array_equal(out[r].cpu().numpy(), exp), (size, r)
             else:
                 nb = size * 4
-                assert algos == ["oneshot" if nb <= 64 << 10 else "direct"] * n, (size, algos)
+                want = "ll" if nb <= 8 << 10 else "oneshot" if nb <= 64 << 10 else "direct"
+                assert algos == [want] * n, (size, algos)
                 exp = vnode.expected_allreduce(orc, data, F32, 0, comms[0])
                 _check([vnode.from_dev(out[r], F32) for r in range(n)], exp)
     finally:
@@ -455,4 +464,40 @@ def test_allgather_oneshot_captured_in_hip_graph():
         _algo(comms, "oneshot")
     finally:
         torch.cuda.synchronize()
+        vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("code,count", [(I8, 1), (I8, 13), (F16, 3), (F16, 4099), (F32, 7), (F64, 5),
+                                        (BF16, 16385), (I32, 65536)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_ll_ragged_and_in_place(orc, code, count, inplace):
+    """LL one-shot words (8 bytes) over ragged buckets: a last partial word
+    (1-byte and 2-byte types), single-element buckets, in place (a thread
+    overwrites only words it has already sent)."""
+    n = 5
+    comms = C.init_all([0] * n, _cfg("ll"))
+    try:
+        rng = np.random.default_rng(count * 3 + code)
+        inputs = [vnode.gen(code, count, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, code, 0, inplace=inplace)
+        _algo(comms, "ll")
+        _check(outs, vnode.expected_allreduce(orc, inputs, code, 0, comms[0]))
+    finally:
+        vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_ll_several_words_per_thread(orc, monkeypatch, inplace):
+    """One workgroup per rank (MCCS_DIRECT_BLOCKS=1): each thread sends and
+    reduces 256 words of a 1 MiB bucket, over the ring's 7 rings at n = 8."""
+    monkeypatch.setenv("MCCS_DIRECT_BLOCKS", "1")
+    n = 8
+    comms = C.init_all([0] * n, _cfg("ll"))
+    try:
+        rng = np.random.default_rng(99)
+        inputs = [vnode.gen(F32, 1 << 18, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, F32, 0, inplace=inplace)
+        _algo(comms, "ll")
+        _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
+    finally:
         vnode.destroy(comms)

@@ -26,7 +26,7 @@ def _free_port() -> int:
 
 @pytest.mark.parametrize("world,modes", [(2, "uncached,device,sender-uncached,sender-device,release,sender-release"),
                                          (4, "uncached,sender-uncached"), (2, "direct,oneshot"),
-                                         (3, "direct,oneshot"), (4, "direct,oneshot")])
+                                         (3, "direct,oneshot,ll"), (4, "direct,oneshot,ll"), (2, "ll")])
 def test_multi_process_ring_matches_oracle(world, modes):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(HERE, "ipc_worker.py")]

@@ -470,3 +470,35 @@ def test_direct_ownership_matches_the_oracle(fake, orc, n, count, rings):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_ll_below_its_threshold(fake):
+    """Buckets up to ll_bytes take the LL one-shot (one 8-byte word per
+    thread: grid = words / 512), larger ones the one-shot; a cached arena
+    (FIFO_DEVICE) never takes LL; the LL slot is exactly 2 x ll_bytes."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(direct_bytes=-1, oneshot_bytes=256 << 10, ll_bytes=32 << 10))
+    cached = None
+    try:
+        for count, want in ((1, "ll"), (1000, "ll"), (8192, "ll"), (8193, "oneshot")):
+            _log()
+            _allreduce_group(comms, count=count)
+            launches = [kv for k, kv in _log() if k == "launch"]
+            assert len(launches) == 8
+            assert all(c.last_algo() == want for c in comms), (count, [c.last_algo() for c in comms])
+            for kv in launches:
+                assert kv["kind"] == "direct" and kv["mode"] == want
+                if want == "ll":
+                    assert int(kv["gx"]) == max(1, (count * 4 + 4095) // 4096)
+                    assert int(kv["llslot"]) == 64 << 10
+        for c in comms:
+            c.sync()
+        cached = C.init_all(list(range(8)), C.CommConfig(direct_bytes=-1, oneshot_bytes=256 << 10, ll_bytes=32 << 10,
+                                                         fifo_memory=C.FIFO_DEVICE))
+        _allreduce_group(cached, count=1000)
+        assert all(c.last_algo() == "oneshot" for c in cached)
+        for c in cached:
+            c.sync()
+    finally:
+        for c in comms + (cached or []):
+            c.destroy()

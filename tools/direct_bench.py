@@ -41,17 +41,20 @@ def main():
     st = side_stream(torch, 0, slot=1)
     for n in args.n:
         top = max(args.sizes_kib) << 10
-        sets = {"ring": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, oneshot_bytes=-1)),
-                "direct": C.init_all([0] * n, C.CommConfig(direct_bytes=top, oneshot_bytes=-1)),
-                "oneshot": C.init_all([0] * n, C.CommConfig(direct_bytes=-1,
-                                                            oneshot_bytes=min(top, args.oneshot_max_kib << 10)))}
+        sets = {"ring": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1)),
+                "direct": C.init_all([0] * n, C.CommConfig(direct_bytes=top, oneshot_bytes=-1, ll_bytes=-1)),
+                "oneshot": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, ll_bytes=-1,
+                                                            oneshot_bytes=min(top, args.oneshot_max_kib << 10))),
+                "ll": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=1 << 20))}
         for kib in args.sizes_kib:
             cnt = (kib << 10) // es
             xs = [torch.randn(cnt, device="cuda").to(dt) for _ in range(n)]
             ys = [torch.empty(n * cnt if args.allgather else cnt, dtype=dt, device="cuda") for _ in xs]
             row = {"n": n, "bytes": kib << 10}
             for algo, comms in sets.items():
-                if algo == "oneshot" and kib > args.oneshot_max_kib:
+                if algo == "oneshot" and kib > args.oneshot_max_kib or algo == "ll" and kib > 1024:
+                    continue
+                if args.allgather and algo == "ll":
                     continue
                 if args.allgather and algo == "direct":
                     continue
