@@ -6,10 +6,11 @@
 Reads every N > 1 bench line (one JSON object per line, or a JSON list) and,
 from its `config.direct_sweep_fp16` table (ring / two-shot / one-shot per
 call at the sweep's sizes, graph replay), prints per N the largest size at
-which one-shot is the fastest of the three and the largest at which two-shot
-still beats the ring -- the values to put into default_oneshot_bytes /
-default_direct_bytes (mccs_amd/csrc/host/api.cpp) -- next to the defaults
-the run used.
+which the LL one-shot is the fastest of all, the largest at which one-shot
+is the fastest of ring / two-shot / one-shot and the largest at which
+two-shot still beats the ring -- the values to put into default_ll_bytes /
+default_oneshot_bytes / default_direct_bytes (mccs_amd/csrc/host/api.cpp)
+-- next to the defaults the run used.
 """
 import json
 import sys
@@ -34,18 +35,22 @@ def lines(path):
 
 def recommend(sweep):
     rows = sweep.get("rows", [])
-    oneshot = direct = 0
+    ll = oneshot = direct = 0
     for r in rows:
         ring = r.get("ring_graph_us", r.get("ring_us"))
         d = r.get("direct_graph_us", r.get("direct_us"))
         o = r.get("oneshot_graph_us", r.get("oneshot_us"))
+        q = r.get("ll_graph_us", r.get("ll_us"))
         if ring is None:
             continue
+        others = [x for x in (ring, d, o) if x is not None]
+        if q is not None and q <= min(others):
+            ll = r["bytes"]
         if o is not None and o <= min(ring, d if d is not None else ring):
             oneshot = r["bytes"]
         if d is not None and d < ring:
             direct = r["bytes"]
-    return oneshot, direct
+    return ll, oneshot, direct
 
 
 def main(paths):
@@ -54,10 +59,10 @@ def main(paths):
             sweep = (d.get("config") or {}).get("direct_sweep_fp16")
             if not sweep:
                 continue
-            o, t = recommend(sweep)
+            q, o, t = recommend(sweep)
             used = (sweep.get("summary") or {}).get("default_thresholds")
             print(json.dumps({"file": p, "n_gpus": d.get("n_gpus"), "p2p_atomics": sweep.get("p2p_atomics"),
-                              "failed": sweep.get("failed"), "recommend_oneshot_bytes": o,
+                              "failed": sweep.get("failed"), "recommend_ll_bytes": q, "recommend_oneshot_bytes": o,
                               "recommend_direct_bytes": t, "defaults_used": used}))
 
 
