@@ -144,7 +144,7 @@ typedef struct {
                            every chunk itself (same order, same bits; one exchange instead of
                            two).  0 = default (MCCS_ONESHOT_BYTES; else 2 MiB at 2 ranks, 1 MiB at
                            3-4, 256 KiB above), < 0 = never; ranks must agree */
-  int ll_bytes;         /* AllReduce buckets of at most this many bytes per rank take the LL one-shot
+  int ll_bytes;         /* AllReduce / AllGather buckets of at most this many bytes per rank take the LL one-shot
                            (flag-carrying 16-byte lines: no drain, no count atomic) when the arena is
                            uncached; same order, same bits.  0 = default (MCCS_LL_BYTES; else 128 KiB),
                            < 0 = never, at most 1 MiB; ranks must agree (appended in 0.3.1) */

@@ -603,10 +603,15 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
                          2 * (int64_t)MCCS_DIRECT_MAX_RANKS * (int64_t)a.oslot_bytes +
                          (int64_t)(seq & 1) * MCCS_DIRECT_MAX_RANKS * lslot;
   bool ok = s_ok != 0;
+  const bool ag = a.mode == MCCS_DIRECT_LL_AG;  // AllGather: T = int8, w.size = bytes per rank
+  char* const own_seg = out + (int64_t)rank * w.size;
+  const bool own_al = ((uintptr_t)own_seg & 7) == 0;
   // 1. every word to every peer's LL slot, as a flag-carrying line
+  // (AllGather: and to this rank's own place in the output, unless in place)
   if (ok)
     for (uint32_t wd = gtid; wd < nwords; wd += stride) {
       const uint64_t v = wd == gtid ? own0 : ll_load_word<T>(in, wd, w.size, in_al);
+      if (ag && own_seg != in) ll_store_word<T>(own_seg, wd, w.size, own_al, v);
       const uint64_t lo = flag | (v & 0xffffffffull), hi = flag | (v >> 32);
 #pragma unroll
       for (uint32_t t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
@@ -627,13 +632,18 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
   const uint32_t parts = w.nch * n;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t wd = gtid; ok && wd < nwords; wd += stride) {
-    const uint32_t e = wd * EPW;
-    const uint32_t g = e / w.loopSize * w.loopSize;
-    uint32_t rcs = (w.size - g + parts - 1) / parts;  // realChunkSize, all_reduce.h:30-36
-    rcs = w.chunkSize < rcs ? w.chunkSize : rcs;
-    rcs = (rcs + w.gran - 1) / w.gran * w.gran;
-    const uint32_t c = (e - g) / rcs, bid = c / n, k = c - bid * n;
-    const uint64_t own = wd == gtid ? own0 : ll_load_word<T>(in, wd, w.size, in_al);
+    uint32_t bid = 0, k = 0;
+    if (!ag) {
+      const uint32_t e = wd * EPW;
+      const uint32_t g = e / w.loopSize * w.loopSize;
+      uint32_t rcs = (w.size - g + parts - 1) / parts;  // realChunkSize, all_reduce.h:30-36
+      rcs = w.chunkSize < rcs ? w.chunkSize : rcs;
+      rcs = (rcs + w.gran - 1) / w.gran * w.gran;
+      const uint32_t c = (e - g) / rcs;
+      bid = c / n;
+      k = c - bid * n;
+    }
+    const uint64_t own = ag ? 0 : wd == gtid ? own0 : ll_load_word<T>(in, wd, w.size, in_al);
     const char* lb = mine + llbase + (int64_t)wd * 16;
     uint64_t h0[MCCS_DIRECT_MAX_RANKS], h1[MCCS_DIRECT_MAX_RANKS];
     uint32_t pending = peers, spins = 0;
@@ -662,6 +672,16 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
       __builtin_amdgcn_s_sleep(MCCS_POLL_SLEEP);
     }
     if (!ok) break;
+    if (ag) {  // every peer's word to its place (all_gather.h: rank t's segment at t x size)
+#pragma unroll
+      for (uint32_t t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
+        if (t < n && t != rank) {
+          char* seg = out + (int64_t)t * w.size;
+          ll_store_word<T>(seg, wd, w.size, ((uintptr_t)seg & 7) == 0,
+                           (h0[t] & 0xffffffffull) | (h1[t] << 32));
+        }
+      continue;
+    }
     // acc = x[idx k+1]; acc = fn(x[idx k+j], acc)
     u32x4 acc{};
 #pragma unroll
@@ -682,7 +702,7 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
 
 template <int DT, int OP>
 __global__ void __launch_bounds__(MCCS_DIRECT_THREADS) direct_kernel(mccsDirectArgs a) {
-  if (a.mode == MCCS_DIRECT_LL_ONE_SHOT) direct_ll_body<DT, OP>(a);
+  if (a.mode == MCCS_DIRECT_LL_ONE_SHOT || a.mode == MCCS_DIRECT_LL_AG) direct_ll_body<DT, OP>(a);
   else direct_body<DT, OP>(a);
 }
 

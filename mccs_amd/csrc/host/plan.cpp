@@ -129,7 +129,7 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   const size_t bytes = func == mccsFuncAllGather ? count : count * (size_t)elem_bytes(dtype);
   const bool oneshot = c->layout.oneshot_slot > 0 && bytes <= (size_t)c->cfg.oneshot_bytes;
   const bool twoshot = func == mccsFuncAllReduce && c->layout.direct_slot > 0 && bytes <= (size_t)c->cfg.direct_bytes;
-  const bool ll = func == mccsFuncAllReduce && ll_fits(c, bytes);
+  const bool ll = ll_fits(c, bytes);
   if (!c->plan_pending && (func == mccsFuncAllReduce || func == mccsFuncAllGather) && c->direct_ok &&
       (oneshot || twoshot || ll)) {
     c->plan_direct = true;
@@ -457,10 +457,10 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   da->oslot_bytes = c0->layout.oneshot_slot;
   da->ll_slot_bytes = c0->layout.ll_slot;
   const size_t nbytes = (size_t)c0->direct.count * esize;
-  bool ll = !gather;  // every rank slot of the launch must take it (uncached arena)
+  bool ll = true;  // every rank slot of the launch must take it (uncached arena)
   for (size_t k = 0; k < idx.size(); ++k) ll = ll && ll_fits(comms[idx[k]], nbytes);
   const bool oneshot = ll || (c0->layout.oneshot_slot > 0 && nbytes <= (size_t)c0->cfg.oneshot_bytes);
-  da->mode = gather ? MCCS_DIRECT_AG_ONE_SHOT
+  da->mode = gather ? (ll ? MCCS_DIRECT_LL_AG : MCCS_DIRECT_AG_ONE_SHOT)
              : ll   ? MCCS_DIRECT_LL_ONE_SHOT
              : oneshot ? MCCS_DIRECT_ONE_SHOT
                        : MCCS_DIRECT_TWO_SHOT;
@@ -690,7 +690,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       comms[idx[k]]->event_recorded = record;
       comms[idx[k]]->last_algo = !direct                            ? MCCS_ALGO_RING
                                  : da.mode == MCCS_DIRECT_TWO_SHOT ? MCCS_ALGO_DIRECT
-                                 : da.mode == MCCS_DIRECT_LL_ONE_SHOT ? MCCS_ALGO_LL
+                                 : da.mode == MCCS_DIRECT_LL_ONE_SHOT || da.mode == MCCS_DIRECT_LL_AG ? MCCS_ALGO_LL
                                                                    : MCCS_ALGO_ONESHOT;
     }
     c0->event_recorded = record || stop_on_launch;

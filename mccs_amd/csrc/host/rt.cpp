@@ -241,6 +241,7 @@ class FakeRuntime final : public DeviceRuntime {
                 " mode=" + (da->mode == MCCS_DIRECT_ONE_SHOT      ? "oneshot"
                             : da->mode == MCCS_DIRECT_AG_ONE_SHOT ? "ag-oneshot"
                             : da->mode == MCCS_DIRECT_LL_ONE_SHOT ? "ll"
+                            : da->mode == MCCS_DIRECT_LL_AG       ? "ll-ag"
                                                                   : "twoshot") +
                 " gx=" + std::to_string(grid.x) + " llslot=" + std::to_string(da->ll_slot_bytes) +
                 " piece=" + std::to_string(da->piece) + " piece2=" + std::to_string(da->piece2) + " owned=";

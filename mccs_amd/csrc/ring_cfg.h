@@ -169,6 +169,7 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 #define MCCS_DIRECT_ONE_SHOT 1
 #define MCCS_DIRECT_AG_ONE_SHOT 2  // AllGather: count = bytes per rank (dtype int8)
 #define MCCS_DIRECT_LL_ONE_SHOT 3  // one-shot through flag-carrying 16-byte lines (uncached arenas)
+#define MCCS_DIRECT_LL_AG 4        // AllGather through the same lines (count = bytes per rank)
 
 struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
   const void* send;

@@ -360,19 +360,21 @@ def _allgather(comms, bufs_in, nbytes, inplace):
 @pytest.mark.parametrize("inplace", [False, True])
 @pytest.mark.parametrize("n", [2, 3, 8])
 @pytest.mark.parametrize("nbytes", [1, 1000, 4096, 65539, 1 << 20])
-def test_allgather_oneshot(n, nbytes, inplace):
-    """AllGather buckets up to oneshot_bytes take the one-shot exchange: every
-    rank's segment lands in every output byte for byte (all_gather.h's
-    result), in place (allgather_proto's layout) or not."""
+@pytest.mark.parametrize("variant", ["oneshot", "ll"])
+def test_allgather_oneshot(n, nbytes, inplace, variant):
+    """AllGather buckets up to oneshot_bytes take the one-shot exchange (up
+    to ll_bytes its LL lines): every rank's segment lands in every output
+    byte for byte (all_gather.h's result), in place (allgather_proto's
+    layout) or not."""
     import torch
 
-    comms = C.init_all([0] * n, _cfg("oneshot"))
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(nbytes + n)
         data = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(n)]
         bufs = [torch.from_numpy(d).cuda() for d in data]
         outs = _allgather(comms, bufs, nbytes, inplace)
-        _algo(comms, "oneshot")
+        _algo(comms, variant)
         exp = np.concatenate(data)
         for r, o in enumerate(outs):
             assert np.array_equal(o, exp), f"rank {r}"
@@ -415,7 +417,8 @@ def test_allgather_oneshot_back_to_back_and_mixed(orc):
             c.sync()
         for kind, size, data, src, out, algos in keep:
             if kind == "ag":
-                assert algos == ["oneshot" if size <= 64 << 10 else "ring"] * n, (size, algos)
+                want = "ll" if size <= 8 << 10 else "oneshot" if size <= 64 << 10 else "ring"
+                assert algos == [want] * n, (size, algos)
                 exp = np.concatenate(data)
                 for r in range(n):
                     assert np.array_equal(out[r].cpu().numpy(), exp), (size, r)
@@ -429,11 +432,12 @@ def test_allgather_oneshot_back_to_back_and_mixed(orc):
         vnode.destroy(comms)
 
 
-def test_allgather_oneshot_captured_in_hip_graph():
+@pytest.mark.parametrize("variant", ["oneshot", "ll"])
+def test_allgather_oneshot_captured_in_hip_graph(variant):
     import torch
 
     n, size = 3, 40000
-    comms = C.init_all([0] * n, _cfg("oneshot"))
+    comms = C.init_all([0] * n, _cfg(variant))
     try:
         rng = np.random.default_rng(5)
         src = [torch.zeros(size, dtype=torch.uint8, device="cuda") for _ in range(n)]
@@ -461,7 +465,7 @@ def test_allgather_oneshot_captured_in_hip_graph():
             exp = np.concatenate(data)
             for r in range(n):
                 assert np.array_equal(out[r].cpu().numpy(), exp), (it, r)
-        _algo(comms, "oneshot")
+        _algo(comms, variant)
     finally:
         torch.cuda.synchronize()
         vnode.destroy(comms)

@@ -502,3 +502,24 @@ def test_ll_below_its_threshold(fake):
     finally:
         for c in comms + (cached or []):
             c.destroy()
+
+
+def test_ll_allgather_plans(fake):
+    """AllGathers up to ll_bytes per rank take the LL lines (mode ll-ag),
+    larger ones up to oneshot_bytes the one-shot exchange."""
+    fake(8)
+    comms = C.init_all(list(range(8)), C.CommConfig(oneshot_bytes=64 << 10, direct_bytes=-1, ll_bytes=16 << 10))
+    try:
+        for nbytes, want, mode in ((1000, "ll", "ll-ag"), (16 << 10, "ll", "ll-ag"), ((16 << 10) + 1, "oneshot", "ag-oneshot")):
+            _log()
+            with C.group():
+                for r, c in enumerate(comms):
+                    C.all_gather(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, nbytes, stream=0)
+            launches = [kv for k, kv in _log() if k == "launch"]
+            assert launches and all(kv["mode"] == mode for kv in launches), (nbytes, launches[:1])
+            assert all(c.last_algo() == want for c in comms)
+        for c in comms:
+            c.sync()
+    finally:
+        for c in comms:
+            c.destroy()

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--calls", type=int, default=100)
     ap.add_argument("--dtype", default="float16")
     ap.add_argument("--oneshot-max-kib", type=int, default=2048)
+    ap.add_argument("--algos", nargs="+", default=["ring", "direct", "oneshot", "ll"],
+                    help="variants to time (rocprof passes isolate one kernel mode each)")
     ap.add_argument("--allgather", action="store_true", help="time AllGather (size = bytes per rank): ring vs one-shot")
     args = ap.parse_args()
     dt = getattr(torch, args.dtype)
@@ -46,6 +48,9 @@ def main():
                 "oneshot": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, ll_bytes=-1,
                                                             oneshot_bytes=min(top, args.oneshot_max_kib << 10))),
                 "ll": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=1 << 20))}
+        for a in [a for a in sets if a not in args.algos]:
+            for c in sets.pop(a):
+                c.destroy()
         for kib in args.sizes_kib:
             cnt = (kib << 10) // es
             xs = [torch.randn(cnt, device="cuda").to(dt) for _ in range(n)]

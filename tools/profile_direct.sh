@@ -9,7 +9,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_direct" -o trace \
+TAG=${DIRECT_TAG:-direct}
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_$TAG" -o trace \
   -- python3 "$R/tools/direct_bench.py" --n ${DIRECT_N:-8} --sizes-kib ${DIRECT_KIB:-32 512 2048} --blocks 128 \
-  --calls 50 > "$OUT/prof_direct.log" 2>&1 || { echo "direct trace failed $?"; exit 3; }
+  --calls 50 --algos ${DIRECT_ALGOS:-ring direct oneshot ll} > "$OUT/prof_$TAG.log" 2>&1 || { echo "direct trace failed $?"; exit 3; }
 echo "direct profile done"
