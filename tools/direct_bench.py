@@ -59,8 +59,6 @@ def main():
             for algo, comms in sets.items():
                 if algo == "oneshot" and kib > args.oneshot_max_kib or algo == "ll" and kib > 1024:
                     continue
-                if args.allgather and algo == "ll":
-                    continue
                 if args.allgather and algo == "direct":
                     continue
                 for blocks in (args.blocks if algo != "ring" else [0]):
