@@ -294,19 +294,20 @@ class HostRingPool {
   }
 
   // Task 0 runs on the calling thread; tasks 1.. go to parked workers 1..
-  // (a 2-rank call wakes one worker).  The job is published through gen_
-  // (release) and picked up with an acquire load, so a spinning worker
-  // starts without touching the mutex.
+  // (a 2-rank call wakes one worker).  The job, its task count and the
+  // generation change together under mu_, and a worker reads them together
+  // under mu_, so a worker that lagged behind a call it had no task in
+  // cannot pair an old generation with a newer job.
   void run(Ctx* c, int ntasks) {
     while ((int)workers_.size() < ntasks - 1) {
       const int id = (int)workers_.size() + 1;
       workers_.emplace_back([this, id] { loop(id); });
     }
     remaining_.store(ntasks - 1, std::memory_order_relaxed);
-    job_.store(c, std::memory_order_relaxed);
-    ntasks_.store(ntasks, std::memory_order_relaxed);
     {
-      std::lock_guard<std::mutex> lk(mu_);  // pairs with a sleeper's predicate check
+      std::lock_guard<std::mutex> lk(mu_);  // also pairs with a sleeper's predicate check
+      job_.store(c, std::memory_order_relaxed);
+      ntasks_.store(ntasks, std::memory_order_relaxed);
       gen_.fetch_add(1, std::memory_order_release);
     }
     if (sleepers_.load(std::memory_order_acquire)) cv_.notify_all();
@@ -333,9 +334,14 @@ class HostRingPool {
         cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
         sleepers_.fetch_sub(1, std::memory_order_acq_rel);
       }
-      seen = gen_.load(std::memory_order_acquire);
-      Ctx* c = job_.load(std::memory_order_relaxed);
-      const int ntasks = ntasks_.load(std::memory_order_relaxed);
+      Ctx* c;
+      int ntasks;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        seen = gen_.load(std::memory_order_acquire);
+        c = job_.load(std::memory_order_relaxed);
+        ntasks = ntasks_.load(std::memory_order_relaxed);
+      }
       if (id < ntasks) {
         run_rank_channel(c, id / c->nch, id % c->nch);
         remaining_.fetch_sub(1, std::memory_order_acq_rel);

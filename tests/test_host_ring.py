@@ -58,3 +58,19 @@ def test_host_ring_kat():
     C.host_ring_allreduce(ins, outs, count, 2, 0, channels=2, nthreads=544, buffer_size=1 << 16)
     for o in outs:
         assert np.all(o == 2042 * n + n * (n - 1) // 2)
+
+
+def test_host_ring_pool_across_changing_shapes():
+    """Back-to-back calls whose task counts grow and shrink (2x1 .. 8x2
+    tasks): parked workers without a task in one call must not run the next
+    call's task twice or miss it; every sum exact (integer-valued fp32)."""
+    rng = np.random.default_rng(5)
+    shapes = [(2, 1), (8, 2), (3, 1), (5, 2), (2, 2), (8, 1), (4, 1)]
+    for it in range(140):
+        n, nch = shapes[it % len(shapes)]
+        count = int(rng.integers(1, 3000))
+        send = [rng.integers(-64, 64, count).astype(np.float32) for _ in range(n)]
+        recv = [np.empty_like(x) for x in send]
+        C.host_ring_allreduce(send, recv, count, C.AllReduceDataType.Float32, channels=nch, nthreads=96)
+        exp = np.sum(send, axis=0, dtype=np.float32)
+        assert all(np.array_equal(r, exp) for r in recv), (it, n, nch)
