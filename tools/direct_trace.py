@@ -44,9 +44,9 @@ def main():
     rows = []
     for n in a.n:
         cap = max(a.kib) << 10
-        for variant, kw in (("direct", dict(direct_bytes=cap, oneshot_bytes=-1)),
-                            ("direct-cached", dict(direct_bytes=cap, oneshot_bytes=-1, fifo_memory=C.FIFO_DEVICE)),
-                            ("oneshot", dict(direct_bytes=-1, oneshot_bytes=min(cap, 64 << 20)))):
+        for variant, kw in (("direct", dict(direct_bytes=cap, oneshot_bytes=-1, ll_bytes=-1)),
+                            ("direct-cached", dict(direct_bytes=cap, oneshot_bytes=-1, ll_bytes=-1, fifo_memory=C.FIFO_DEVICE)),
+                            ("oneshot", dict(direct_bytes=-1, oneshot_bytes=min(cap, 64 << 20), ll_bytes=-1))):
             comms = C.init_all([0] * n, C.CommConfig(**kw))
             for kib in a.kib:
                 cnt = (kib << 10) // 2

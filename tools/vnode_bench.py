@@ -35,8 +35,10 @@ def main():
         os.environ["MCCS_RING_PROFILE"] = "1"
     for n in args.n:
         for lanes in args.lanes:
+            # the ring at every size (the direct kernel has tools/direct_bench.py)
             comms = C.init_all([0] * n, C.CommConfig(lanes=lanes, block_threads=args.block,
-                                                          bridge_streams=args.bridge or None))
+                                                          bridge_streams=args.bridge or None,
+                                                          direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1))
             for kib in (args.sizes_kib or [m << 10 for m in args.sizes_mib]):
                 cnt = (kib << 10) // 4
                 xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
