@@ -203,7 +203,8 @@ int mccsCommLastAlgo(mccsComm_t comm);
 /* 1 when the comm may run the direct kernel: a direct region was configured
  * and every device of the communicator can perform atomics on every other's
  * memory (hipDevP2PAttrNativeAtomicSupported; the hand-off counts are remote
- * atomics).  Otherwise every AllReduce takes the ring. */
+ * atomics).  Otherwise every AllReduce takes the ring, except buckets up to
+ * ll_bytes, whose LL one-shot makes no remote atomics. */
 int mccsCommDirectEnabled(mccsComm_t comm);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);

@@ -130,8 +130,10 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   const bool oneshot = c->layout.oneshot_slot > 0 && bytes <= (size_t)c->cfg.oneshot_bytes;
   const bool twoshot = func == mccsFuncAllReduce && c->layout.direct_slot > 0 && bytes <= (size_t)c->cfg.direct_bytes;
   const bool ll = ll_fits(c, bytes);
-  if (!c->plan_pending && (func == mccsFuncAllReduce || func == mccsFuncAllGather) && c->direct_ok &&
-      (oneshot || twoshot || ll)) {
+  // (the LL one-shot makes no remote atomics: it runs without peer atomics,
+  // the count-based variants need them)
+  if (!c->plan_pending && (func == mccsFuncAllReduce || func == mccsFuncAllGather) &&
+      ((c->direct_ok && (oneshot || twoshot)) || ll)) {
     c->plan_direct = true;
     c->direct.send = send;
     c->direct.recv = recv;
@@ -459,6 +461,7 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   const size_t nbytes = (size_t)c0->direct.count * esize;
   bool ll = true;  // every rank slot of the launch must take it (uncached arena)
   for (size_t k = 0; k < idx.size(); ++k) ll = ll && ll_fits(comms[idx[k]], nbytes);
+  if (!ll && !c0->direct_ok) return mccsInternalError;  // plan_enqueue held it for LL only
   const bool oneshot = ll || (c0->layout.oneshot_slot > 0 && nbytes <= (size_t)c0->cfg.oneshot_bytes);
   da->mode = gather ? (ll ? MCCS_DIRECT_LL_AG : MCCS_DIRECT_AG_ONE_SHOT)
              : ll   ? MCCS_DIRECT_LL_ONE_SHOT

@@ -401,7 +401,8 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
         cfg = dataclasses.replace(config or C.CommConfig(), **kw)
         try:
             comms[algo] = C.init_communicator_rank(rank, world, device, exchange, cfg)
-            ok = comms[algo].direct_enabled()
+            # the LL one-shot needs no peer atomics (no remote atomics at all)
+            ok = algo == "ll" or comms[algo].direct_enabled()
             err = None if ok else "direct kernel disabled: no peer atomics between these devices"
         except Exception as e:  # noqa: BLE001
             ok, err = False, f"{type(e).__name__}: {e}"[:200]

@@ -523,3 +523,25 @@ def test_ll_allgather_plans(fake):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_ll_runs_without_peer_atomics(fake, monkeypatch):
+    """Without peer atomics the count-based direct variants are off, but the
+    LL one-shot (no remote atomics) still takes the buckets up to ll_bytes;
+    larger ones the ring."""
+    monkeypatch.setenv("MCCS_TEST_NO_P2P_ATOMICS", "1")
+    fake(2)
+    comms = C.init_all([0, 1], C.CommConfig(ll_bytes=64 << 10))
+    try:
+        assert not any(c.direct_enabled() for c in comms)
+        for count, want in ((1000, "ll"), (16384, "ll"), (16385, "ring")):
+            _log()
+            _allreduce_group(comms, count=count)
+            kinds = [kv.get("mode", kv["kind"]) for k, kv in _log() if k == "launch"]
+            assert kinds == (["ll"] * 2 if want == "ll" else ["ring"] * 2), (count, kinds)
+            assert [c.last_algo() for c in comms] == [want] * 2
+        for c in comms:
+            c.sync()
+    finally:
+        for c in comms:
+            c.destroy()
