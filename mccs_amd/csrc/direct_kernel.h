@@ -597,7 +597,10 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
     arrived = __hip_atomic_fetch_add((uint32_t*)(mine + MCCS_DIRECT_DONE), 1u, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t seq = s_seq;
-  const uint64_t flag = (uint64_t)(uint32_t)seq << 32;
+  // 32-bit line flag, never 0 (the region's zeroed lines never read as
+  // valid, whatever the launch count): 1 + seq mod (2^32 - 1)
+  const uint32_t seq32 = 1u + (uint32_t)(seq % 0xffffffffull);
+  const uint64_t flag = (uint64_t)seq32 << 32;
   const int64_t lslot = (int64_t)a.ll_slot_bytes;
   const int64_t llbase = MCCS_DIRECT_CTRL_BYTES + (int64_t)MCCS_DIRECT_SLOTS * (int64_t)a.slot_bytes +
                          2 * (int64_t)MCCS_DIRECT_MAX_RANKS * (int64_t)a.oslot_bytes +
@@ -628,7 +631,6 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
   }
   // 2. poll every peer's line of each word, reduce in the ring's order
   const uint32_t peers = ((1u << n) - 1u) & ~(1u << rank);
-  const uint32_t seq32 = (uint32_t)seq;
   const uint32_t parts = w.nch * n;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t wd = gtid; ok && wd < nwords; wd += stride) {

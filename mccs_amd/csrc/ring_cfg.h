@@ -121,7 +121,8 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must s
 //   [LL one-shot : 2 parities x MCCS_DIRECT_MAX_RANKS senders x ll_slot_bytes]
 // LL one-shot (the smallest buckets): every 8 data bytes travel as one
 // 16-byte line {data lo, flag, data hi, flag} written with two 8-byte
-// system-scope stores, flag = the launch seq; a receiver polls the lines
+// system-scope stores, flag = 1 + seq mod (2^32 - 1) (never 0, so a zeroed
+// line is never valid); a receiver polls the lines
 // themselves, so the hand-off needs no drain, no count atomic and no
 // separate flag round trip.  Its region is written only with such lines
 // (zero at init), so a line left from an earlier launch carries a smaller
