@@ -27,10 +27,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5000)
     ap.add_argument("--size-mib", type=int, default=128)
+    ap.add_argument("--size-kib", type=int, default=0, help="bucket in KiB (overrides --size-mib; small buckets "
+                    "take the library's direct / LL kernels)")
     ap.add_argument("--check-every", type=int, default=1000)
     ap.add_argument("--vnode", type=int, default=0, help="n ranks on cuda:0 in this process")
     args = ap.parse_args()
-    n = (args.size_mib << 20) // 4
+    n = ((args.size_kib << 10) if args.size_kib else (args.size_mib << 20)) // 4
     code = C.AllReduceDataType.Float32
     dev = torch.device("cuda", 0)
     t0 = time.perf_counter()
@@ -56,6 +58,7 @@ def main():
                     ys[r].zero_()
                 checks += 1
                 print(json.dumps({"iteration": it, "ok": True}), flush=True)
+        algo = comms[0].last_algo()
         for c in comms:
             c.destroy()
         rank = 0
@@ -79,12 +82,13 @@ def main():
                 checks += 1
                 if rank == 0:
                     print(json.dumps({"iteration": it, "ok": True}), flush=True)
+        algo = comm.last_algo()
         comm.destroy()
         dist.destroy_process_group()
     if rank == 0:
         el = time.perf_counter() - t0
         print(json.dumps({"soak": "vnode" if args.vnode else "ipc", "ranks": world, "iters": args.iters,
-                          "MiB": args.size_mib, "exact_checks": checks, "seconds": round(el, 1),
+                          "bytes": n * 4, "algo": algo, "exact_checks": checks, "seconds": round(el, 1),
                           "all_exact": True}), flush=True)
 
 
