@@ -48,12 +48,13 @@ def _case(seed):
     if rng.random() < 0.3:
         cfg["fifo_slots"] = int(rng.choice([16, 32]))
     fifo_works = bool(rng.random() < 0.3)  # work list through the FIFO even where it fits the launch arguments
-    # the direct kernel (one-shot / two-shot / AllGather one-shot) at random
+    # the direct kernel (LL / one-shot / two-shot / AllGather one-shot) at random
     # thresholds and workgroup caps; results must not change
     blocks = None
     if rng.random() < 0.5:
         cfg["oneshot_bytes"] = int(rng.choice([-1, 64 << 10, 1 << 20, 8 << 20]))
         cfg["direct_bytes"] = int(rng.choice([-1, 1 << 20, 8 << 20, 32 << 20]))
+        cfg["ll_bytes"] = int(rng.choice([-1, 16 << 10, 128 << 10, 1 << 20]))
         blocks = int(rng.choice([1, 3, 16, 128]))
     return n, code, op, count, cfg, slice2, gather, fifo_works, blocks, rng
 
