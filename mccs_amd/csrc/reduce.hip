@@ -26,6 +26,7 @@
 
 #include "dtypes.h"
 #include "mccs_hip.h"
+#include "lds_dma.h"
 #include "reduce_copy.h"
 
 namespace mccs {
@@ -132,12 +133,6 @@ __global__ void __launch_bounds__(256) reduce_scalar_kernel(ReduceArgs a) {
 // ---------------------------------------------------------------------------
 // LDS: 2 sources -> 1 destination, per-wave LDS-DMA ring of S stages.
 // A wave tile = 64 lanes x U packs per source = U KiB per source.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 // wait until at most nd*G + ns*U vector-memory ops are outstanding
 // (nd, ns < S <= 4; vmcnt immediates must be compile-time constants)
 template <int G, int U, int S>
@@ -154,28 +149,6 @@ __device__ __forceinline__ void wait_younger(int nd, int ns) {
     default: wait_vmcnt<0>(); break;
   }
 #undef MCCS_WY
-}
-
-// One lane's 16 bytes of a wave-wide LDS-DMA: LDS dst = M0 + lane*16.
-// NT: non-temporal (streaming) policy on the DMA read.
-template <int POL>
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_wave_base) {
-  uint32_t keep;
-#define MCCS_GLDS(MODS)                                                   \
-  asm volatile(                                                           \
-      "s_mov_b32 %0, m0\n\t"                                              \
-      "s_mov_b32 m0, %2\n\t"                                              \
-      "s_nop 0\n\t"                                                       \
-      "global_load_lds_dwordx4 %1, off " MODS "\n\t"                      \
-      "s_mov_b32 m0, %0"                                                  \
-      : "=&s"(keep)                                                       \
-      : "v"(gsrc), "s"(lds_wave_base)                                     \
-      : "memory")
-  if constexpr (POL == kNonTemporal) MCCS_GLDS("nt");
-  else if constexpr (POL == kNtWriteThrough) MCCS_GLDS("sc1 nt");
-  else if constexpr (POL == kSystemNt) MCCS_GLDS("sc0 sc1 nt");
-  else MCCS_GLDS("");
-#undef MCCS_GLDS
 }
 
 #ifdef MCCS_REDUCE_TRACE

@@ -11,9 +11,19 @@ gets can be timed and its results checked:
   4096-byte RecvBufMeta (tail at offset 0) and one FIFO of buffer_size bytes
   (8 slots of buffer_size/8).  Head lives with the sender, tail with the
   receiver; the FIFO data with the sender (`Locality::Sender`, the reference
-  default) or with the receiver (`mccs.toml [shm] locality`).  Here the
-  memory is device memory of the owning GPU, shared with the peers over IPC
-  -- the xGMI connector that replaces the host-pinned SHM buffers (§8(f) 2);
+  default) or with the receiver (`mccs.toml [shm] locality`).  `fifo`
+  selects the memory:
+    "device" -- device memory of the owning GPU, shared with the peers over
+      IPC: the xGMI connector that replaces the host-pinned SHM buffers
+      (§8(f) 2);
+    "host"   -- the reference's own SHM memory: page-aligned host memory,
+      mlock'ed (transport/shm/buffer.rs:17-26) and registered mapped with
+      hipHostRegister + hipHostGetDevicePointer in every process that
+      touches it (cuda/alloc.rs:59-99, shm/transporter.rs:102-106).  The
+      reference service is one process, so a plain System.alloc suffices
+      there; the ranks here are processes, so each rank's segment is a POSIX
+      shared-memory object that its peers map too.  This is the deployment
+      an UNCHANGED Rust service runs;
 * comm/device.rs:35-183 (CommDevResources::new, conn_info_to_dev):
   mccsDevCommAndChannels, per-channel peers arrays, userRanks,
   ring prev/next/index, abortFlag, workFifoDone (host-mapped,
@@ -58,8 +68,92 @@ def hip() -> ctypes.CDLL:
         h.hipMalloc.argtypes = [ctypes.POINTER(vp), sz]
         h.hipFree.argtypes = [vp]
         h.hipSetDevice.argtypes = [ctypes.c_int]
+        h.hipHostRegister.argtypes = [vp, sz, ctypes.c_uint]
+        h.hipHostUnregister.argtypes = [vp]
         _hip = h
     return _hip
+
+
+_libc = None
+
+
+def libc() -> ctypes.CDLL:
+    global _libc
+    if _libc is None:
+        c = ctypes.CDLL(None, use_errno=True)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        c.shm_open.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint]
+        c.shm_unlink.argtypes = [ctypes.c_char_p]
+        c.ftruncate.argtypes = [ctypes.c_int, ctypes.c_long]
+        c.mmap.argtypes = [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+        c.mmap.restype = vp
+        c.munmap.argtypes = [vp, sz]
+        c.mlock.argtypes = [vp, sz]
+        c.munlock.argtypes = [vp, sz]
+        c.close.argtypes = [ctypes.c_int]
+        _libc = c
+    return _libc
+
+
+PAGE = 4096
+hipHostRegisterMapped = 0x2
+
+
+class HostSegment:
+    """One rank's SHM connector memory as the reference allocates it: page
+    aligned host memory, mlock'ed (buffer.rs:17-26: System.alloc + mlock),
+    registered mapped for the current device (DeviceHostMapped::register,
+    cuda/alloc.rs:59-99).  `create=True` makes the POSIX shm object (zeroed by
+    ftruncate); peers open it by name.  `dev` is the device address the
+    kernels use; `host` the CPU address."""
+
+    def __init__(self, name: str, nbytes: int, create: bool):
+        c = libc()
+        self.name, self.nbytes = name.encode(), (nbytes + PAGE - 1) // PAGE * PAGE
+        self.host = self.dev = None
+        self._fd, self._registered, self._locked, self._owner = -1, False, False, create
+        flags = (0o100 | 0o200 | 2) if create else 2  # O_CREAT|O_EXCL|O_RDWR / O_RDWR
+        self._fd = c.shm_open(self.name, flags, 0o600)
+        if self._fd < 0:
+            raise OSError(ctypes.get_errno(), f"shm_open({name})")
+        try:
+            if create and c.ftruncate(self._fd, self.nbytes) != 0:
+                raise OSError(ctypes.get_errno(), "ftruncate")
+            p = c.mmap(None, self.nbytes, 0x1 | 0x2, 0x01, self._fd, 0)  # PROT_READ|WRITE, MAP_SHARED
+            if p in (None, ctypes.c_void_p(-1).value):
+                raise OSError(ctypes.get_errno(), "mmap")
+            self.host = p
+            # mlock as the reference does; an ordinary user's RLIMIT_MEMLOCK
+            # may refuse it, and hipHostRegister pins the pages anyway
+            self._locked = c.mlock(p, self.nbytes) == 0
+            _ok(hip().hipHostRegister(p, self.nbytes, hipHostRegisterMapped), "hipHostRegister(mapped)")
+            self._registered = True
+            dp = ctypes.c_void_p()
+            _ok(hip().hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(p), 0), "hipHostGetDevicePointer")
+            self.dev = dp.value or p  # cuda/alloc.rs:80-82: fall back to the host address
+        except Exception:
+            self.close()
+            raise
+
+    def unlink(self) -> None:
+        if self._owner:
+            libc().shm_unlink(self.name)
+            self._owner = False
+
+    def close(self) -> None:
+        c = libc()
+        if self._registered:
+            hip().hipHostUnregister(ctypes.c_void_p(self.host))
+            self._registered = False
+        if self.host:
+            if self._locked:
+                c.munlock(ctypes.c_void_p(self.host), self.nbytes)
+            c.munmap(ctypes.c_void_p(self.host), self.nbytes)
+            self.host = None
+        if self._fd >= 0:
+            c.close(self._fd)
+            self._fd = -1
+        self.unlink()
 
 
 def _ok(rc: int, what: str) -> None:
@@ -153,21 +247,30 @@ class RefDrivenRank:
     default the reference ring on every channel."""
 
     def __init__(self, rank: int, n: int, device: int, allgather, nch: int = 2, rings=None,
-                 buff_size: int = 1 << 22, locality: str = "sender"):
-        if not 2 <= n or not 1 <= nch <= abi.MCCS_MAX_NCHANNELS or locality not in ("sender", "receiver"):
+                 buff_size: int = 1 << 22, locality: str = "sender", fifo: str = "device"):
+        if not 2 <= n or not 1 <= nch <= abi.MCCS_MAX_NCHANNELS or locality not in ("sender", "receiver") \
+                or fifo not in ("device", "host"):
             raise ValueError("bad reference-driven configuration")
         self.rank, self.n, self.device, self.nch, self.buff = rank, n, device, nch, buff_size
         self.rings = [list(r) for r in (rings or reference_rings(n, nch))]
         if len(self.rings) != nch or any(sorted(r) != list(range(n)) for r in self.rings):
             raise ValueError("each channel needs a ring over every rank")
-        self.locality = locality
+        self.locality, self.fifo = locality, fifo
         self.lib = L.load()
         h = hip()
         _ok(h.hipSetDevice(device), "hipSetDevice")
-        self._dev_allocs, self._host_allocs, self._opened = [], [], []
+        self._dev_allocs, self._host_allocs, self._opened, self._segs = [], [], [], []
         # -- connector memory: [SendBufMeta][RecvBufMeta][FIFO] per channel, one allocation
         self.stride = 2 * META + buff_size
         self._mine = 0
+        if fifo == "host":
+            self._init_host_connector(allgather)
+        else:
+            self._init_device_connector(allgather)
+        self._build_device_structs()
+
+    def _init_device_connector(self, allgather) -> None:
+        h, rank, n, device, nch = hip(), self.rank, self.n, self.device, self.nch
         # every rank joins the handle exchange even after a local failure (an
         # empty handle), so a peer's error never leaves the others blocked in it
         mine, handle, local_err = ctypes.c_void_p(), (ctypes.c_char * 64)(), None
@@ -195,6 +298,44 @@ class RefDrivenRank:
         except Exception:
             self.close()  # no collective here: the caller agrees on the failure
             raise
+
+    def _init_host_connector(self, allgather) -> None:
+        """Every rank's [SendBufMeta][RecvBufMeta][FIFO] x channels in host
+        memory (the reference SHM transport): this rank creates its segment,
+        then maps and registers every peer's.  Two exchanges, both joined by
+        every rank whatever fails locally: the names, then "all mapped" (after
+        which the names are unlinked; the mappings keep the memory)."""
+        import uuid
+
+        rank, n = self.rank, self.n
+        nbytes = self.stride * self.nch
+        name, local_err = f"/mccs_refdrv_{uuid.uuid4().hex[:16]}_{rank}", None
+        try:
+            self._segs.append(HostSegment(name, nbytes, create=True))
+        except Exception as e:  # noqa: BLE001
+            local_err = e
+        names = allgather("" if local_err else name)
+        self.base = [0] * n
+        if not local_err and all(names):
+            try:
+                for r in range(n):
+                    if r == rank:
+                        self.base[r] = self._segs[0].dev
+                        continue
+                    seg = HostSegment(names[r], nbytes, create=False)
+                    self._segs.append(seg)
+                    self.base[r] = seg.dev
+            except Exception as e:  # noqa: BLE001
+                local_err = e
+        oks = allgather(local_err is None and all(names))
+        for s in self._segs:
+            s.unlink()
+        if not all(oks):
+            self.close()
+            raise RuntimeError(f"reference-driven host connector setup failed ({local_err or 'on another rank'})")
+
+    def _build_device_structs(self) -> None:
+        h, rank, n, nch, buff_size, locality = hip(), self.rank, self.n, self.nch, self.buff, self.locality
         # -- host-mapped sync: work ring + workFifoDone (device.rs:56-64)
         self.h_work, self.d_work = self._host_mapped(abi.MCCS_WORK_SIZE * WORK_DEPTH)
         self.h_done, self.d_done = self._host_mapped(4 * abi.MCCS_MAX_NCHANNELS)
@@ -341,7 +482,7 @@ class RefDrivenRank:
         own, which the peers may still have mapped.  Safe on a partly built
         rank."""
         h = hip()
-        for name in ("_opened", "_dev_allocs", "_host_allocs"):
+        for name in ("_opened", "_dev_allocs", "_host_allocs", "_segs"):
             if not hasattr(self, name):
                 setattr(self, name, [])
         if not hasattr(self, "_mine"):
@@ -350,6 +491,11 @@ class RefDrivenRank:
         for p in self._opened:
             self.lib.mccsMemCloseShared(self.device, ctypes.c_void_p(p))
         self._opened = []
+        # host connector: our mappings only (a peer's pages live on until its
+        # own close unmaps them; every name was unlinked after setup)
+        for s in self._segs:
+            s.close()
+        self._segs = []
         if barrier is not None:
             barrier()
         if self._mine:
@@ -385,9 +531,13 @@ def default_variants(world: int, default_rings, max_channels: int = 32) -> list[
     mccs.toml's channel_count = 2 (the shipped default), MCCS_MAX_NCHANNELS =
     32 on the reference ring, and the same 32-channel budget over this
     library's link-spreading rings given as comm_patterns_override, with the
-    FIFO data at the sender (the reference SHM layout) or the receiver.
-    `max_channels` caps the budget where ranks share one GPU (a rehearsal:
-    every rank's workgroups must be resident at once)."""
+    FIFO data at the sender (the reference SHM layout) or the receiver
+    (`mccs.toml [shm] locality = receiver`, config only).  `fifo`: "device"
+    (the xGMI connector: FIFOs in the owning GPU's HBM) or "host" (the
+    reference's own SHM memory, mlock'ed host pages registered mapped: what
+    an unchanged service allocates).  `max_channels` caps the budget where
+    ranks share one GPU (a rehearsal: every rank's workgroups must be
+    resident at once)."""
     cap = max(2, min(32, max_channels))
     base = default_rings(world, 0)
     uniq = []
@@ -396,11 +546,17 @@ def default_variants(world: int, default_rings, max_channels: int = 32) -> list[
             uniq.append(r)
     spread = (uniq * cap)[:max(1, cap // len(uniq)) * len(uniq)]
     return [
-        {"name": "ch2_reference_ring_sender", "nch": 2, "rings": None, "locality": "sender"},
-        {"name": f"ch{cap}_reference_ring_sender", "nch": cap, "rings": None, "locality": "sender"},
-        {"name": f"ch{len(spread)}_spread_rings_sender", "nch": len(spread), "rings": spread, "locality": "sender"},
+        {"name": "ch2_reference_ring_sender", "nch": 2, "rings": None, "locality": "sender", "fifo": "device"},
+        {"name": "ch2_reference_ring_receiver", "nch": 2, "rings": None, "locality": "receiver", "fifo": "device"},
+        {"name": "ch2_reference_ring_sender_hostfifo", "nch": 2, "rings": None, "locality": "sender",
+         "fifo": "host"},
+        {"name": f"ch{cap}_reference_ring_sender", "nch": cap, "rings": None, "locality": "sender", "fifo": "device"},
+        {"name": f"ch{cap}_reference_ring_sender_hostfifo", "nch": cap, "rings": None, "locality": "sender",
+         "fifo": "host"},
+        {"name": f"ch{len(spread)}_spread_rings_sender", "nch": len(spread), "rings": spread, "locality": "sender",
+         "fifo": "device"},
         {"name": f"ch{len(spread)}_spread_rings_receiver", "nch": len(spread), "rings": spread,
-         "locality": "receiver"},
+         "locality": "receiver", "fifo": "device"},
     ]
 
 
@@ -441,11 +597,12 @@ def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbyte
     # all ranks together.
     out = []
     for v in variants:
-        res = {"variant": v["name"], "channels": v["nch"], "locality": v["locality"]}
+        res = {"variant": v["name"], "channels": v["nch"], "locality": v["locality"],
+               "fifo": v.get("fifo", "device")}
         rr, err = None, None
         try:
             rr = RefDrivenRank(rank, world, device, allgather, nch=v["nch"], rings=v["rings"],
-                               locality=v["locality"])
+                               locality=v["locality"], fifo=v.get("fifo", "device"))
         except Exception as e:  # noqa: BLE001
             err = f"setup: {type(e).__name__}: {e}"[:300]
         if agree(err is None):

@@ -11,7 +11,10 @@ FIFO layout, comm/device.rs, plan.rs's host-mapped work ring with rolling
 acks, get_task_schema and launch_plan: grid = #channels, 544-thread blocks).
 
 Each variant (reference ring with the FIFO at the sender, the reference
-default; a rotated ring override with the FIFO at the receiver) runs four
+default; a rotated ring override with the FIFO at the receiver; both again
+with every SendBufMeta / RecvBufMeta / FIFO in the reference's own SHM
+memory: mlock'ed host pages registered mapped, transport/shm/buffer.rs:17-26,
+cuda/alloc.rs:59-99) runs four
 cases three times each on the same structures (conn->step persists across
 launches, prims_simple.h:318-319,461) and then 1100 back-to-back launches,
 so the 1024-entry work ring wraps and flow-controls on workFifoDone
@@ -50,11 +53,14 @@ def main():
     if os.environ.get("REFDRV_BIG") == "1":
         return big_case(torch, dist, refdrive, orc, rank, n, dev, allgather)
     rot = list(range(1, n)) + [0]
-    variants = [("ref_sender", 2, None, "sender"), ("rotated_receiver", 2, [rot, rot[::-1]], "receiver")]
+    variants = [("ref_sender", 2, None, "sender", "device"),
+                ("rotated_receiver", 2, [rot, rot[::-1]], "receiver", "device"),
+                ("ref_sender_hostfifo", 2, None, "sender", "host"),
+                ("rotated_receiver_hostfifo", 2, [rot, rot[::-1]], "receiver", "host")]
     results = {}
     stream = torch.cuda.Stream()
-    for vname, nch, rings, loc in variants:
-        rr = refdrive.RefDrivenRank(rank, n, dev, allgather, nch=nch, rings=rings, locality=loc)
+    for vname, nch, rings, loc, fifo in variants:
+        rr = refdrive.RefDrivenRank(rank, n, dev, allgather, nch=nch, rings=rings, locality=loc, fifo=fifo)
         for code, count in ((6, 1 << 20), (7, (1 << 21) + 3), (2, 300007), (6, 777777)):
             rng = np.random.default_rng(count + rank)
             for rep in range(3):
@@ -104,7 +110,8 @@ def main():
 def big_case(torch, dist, refdrive, orc, rank, n, dev, allgather):
     """configs[2]'s bucket (128 MiB fp32 per rank), random uniform [-1, 1)
     inputs, reference-driven at the mccs.toml default (2 channels, ring
-    0..n-1) and at 32 channels: every rank's output bit for bit against the
+    0..n-1), at 32 channels, and at 2 channels on host-memory FIFOs (the
+    reference SHM transport's own memory): every rank's output bit for bit against the
     oracle's ring order.  Each process regenerates every rank's inputs from
     the same seeds (no bulk exchange)."""
     import numpy as np
@@ -120,8 +127,8 @@ def big_case(torch, dist, refdrive, orc, rank, n, dev, allgather):
     host = [inputs_of(r).cpu().numpy() for r in range(n)]
     stream = torch.cuda.Stream()
     results = {}
-    for nch in (2, 32):
-        rr = refdrive.RefDrivenRank(rank, n, dev, allgather, nch=nch)
+    for nch, fifo in ((2, "device"), (32, "device"), (2, "host")):
+        rr = refdrive.RefDrivenRank(rank, n, dev, allgather, nch=nch, fifo=fifo)
         recv = torch.empty_like(mine)
         torch.cuda.synchronize()
         dist.barrier()
@@ -134,7 +141,7 @@ def big_case(torch, dist, refdrive, orc, rank, n, dev, allgather):
         naive = host[0].copy()
         for r in range(1, n):
             naive += host[r]
-        results[f"big/ch{nch}"] = {"ok": bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        results[f"big/ch{nch}/{fifo}"] = {"ok": bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
                                    and not rr.aborted() and (n < 3 or not np.array_equal(naive, want)),
                                    "steps": rr.steps(), "grid": k, "block": nthr}
         rr.close(dist.barrier)

@@ -103,26 +103,73 @@ def test_work_ring_counters_wrap_u32():
 def test_configuration_only_variants(n):
     vs = refdrive.default_variants(n, C.default_rings)
     names = [v["name"] for v in vs]
-    assert names[0] == "ch2_reference_ring_sender" and names[1] == "ch32_reference_ring_sender"
+    assert names[:5] == ["ch2_reference_ring_sender", "ch2_reference_ring_receiver",
+                         "ch2_reference_ring_sender_hostfifo", "ch32_reference_ring_sender",
+                         "ch32_reference_ring_sender_hostfifo"]
+    # the shipped 2-channel shape under each config-only choice: locality and
+    # the reference's own host-memory FIFOs
+    assert [(v["locality"], v["fifo"]) for v in vs[:3]] == [("sender", "device"), ("receiver", "device"),
+                                                           ("sender", "host")]
     for v in vs:
-        assert 1 <= v["nch"] <= 32 and v["locality"] in ("sender", "receiver")
+        assert 1 <= v["nch"] <= 32 and v["locality"] in ("sender", "receiver") and v["fifo"] in ("device", "host")
         if v["rings"] is not None:
             assert len(v["rings"]) == v["nch"]
             for r in v["rings"]:
                 assert sorted(r) == list(range(n))
-    spread = vs[2]["rings"]
+    spread = vs[5]["rings"]
     # the spread variants cycle over every distinct default ring equally often
     uniq = {tuple(r) for r in spread}
     assert all(sum(1 for r in spread if tuple(r) == u) == len(spread) // len(uniq) for u in uniq)
     if n == 8:
-        assert len(uniq) == 7 and vs[2]["nch"] == 28
+        assert len(uniq) == 7 and vs[5]["nch"] == 28
 
 
 def test_variants_capped_when_ranks_share_a_gpu():
     vs = refdrive.default_variants(8, C.default_rings, 16)
-    assert [v["nch"] for v in vs] == [2, 16, 14, 14]
+    assert [v["nch"] for v in vs] == [2, 2, 2, 16, 16, 14, 14]
     assert all(v["nch"] * 8 <= 128 for v in vs)
 
 
 def test_reference_rings_are_the_engine_default():
     assert refdrive.reference_rings(4, 2) == [[0, 1, 2, 3], [0, 1, 2, 3]]
+
+
+def test_host_segment_roundtrip_without_gpu(monkeypatch):
+    """The host connector's segment: shm_open + ftruncate (zeroed) + mmap +
+    mlock, registered through hipHostRegister (faked here: no GPU); a peer
+    opening the name sees the creator's bytes; the name is unlinked once
+    every rank mapped it."""
+    import ctypes
+    import uuid
+
+    calls = []
+
+    class FakeHip:
+        def hipHostRegister(self, p, n, flags):
+            calls.append(("reg", n, flags))
+            return 0
+
+        def hipHostGetDevicePointer(self, out, p, flags):
+            out._obj.value = p.value
+            return 0
+
+        def hipHostUnregister(self, p):
+            calls.append(("unreg",))
+            return 0
+
+    monkeypatch.setattr(refdrive, "hip", lambda: FakeHip())
+    name = f"/mccs_test_{uuid.uuid4().hex[:12]}"
+    a = refdrive.HostSegment(name, 3 * 4096 + 5, create=True)
+    try:
+        assert a.nbytes == 4 * 4096 and a.dev == a.host
+        assert bytes((ctypes.c_char * 64).from_address(a.host)) == bytes(64)
+        ctypes.memset(a.host + 4096, 0x5A, 16)
+        b = refdrive.HostSegment(name, 3 * 4096 + 5, create=False)
+        assert bytes((ctypes.c_char * 16).from_address(b.host + 4096)) == b"\x5a" * 16
+        a.unlink()
+        with pytest.raises(OSError):
+            refdrive.HostSegment(name, 4096, create=False)
+        b.close()
+    finally:
+        a.close()
+    assert calls.count(("reg", 4 * 4096, refdrive.hipHostRegisterMapped)) == 2 and calls.count(("unreg",)) == 2
