@@ -113,9 +113,12 @@ typedef struct mccsComm *mccsComm_t;
 /* Communicator profile: comm_default_config (mccs.toml:18-20, config.rs:15-97)
  * plus the MI355X execution knobs.  Zero fields take defaults.
  * ABI note: `fifo_slots`, `direct_bytes` and `oneshot_bytes` were appended in
- * library version 0.3, which grew the struct; mccsCommConfigDefault() writes sizeof(mccsCommConfig) bytes, so a
- * caller compiled against an older header must be rebuilt.  Callers binding
- * the struct by hand (ctypes, bindgen) check mccsCommConfigSize(). */
+ * library version 0.3 and `ll_bytes` in 0.3.1, which grew the struct;
+ * mccsCommConfigDefault() writes sizeof(mccsCommConfig) bytes, so a caller
+ * compiled against an older header must be rebuilt.  From 0.4 the struct ends
+ * in reserved words that later fields will take, so its size stays fixed;
+ * callers binding the struct by hand (ctypes, bindgen) check
+ * mccsCommConfigSize() or call mccsCommConfigDefaultSized(). */
 typedef struct {
   int channel_count;    /* rings; 0 = auto: 2 x edge-disjoint Hamiltonian cycles of the node */
   int buffer_size;      /* FIFO bytes per connection (buffer_sizes[0]); 0 = 4 MiB */
@@ -148,11 +151,18 @@ typedef struct {
                            (flag-carrying 16-byte lines: no drain, no count atomic) when the arena is
                            uncached; same order, same bits.  0 = default (MCCS_LL_BYTES; else 128 KiB),
                            < 0 = never, at most 1 MiB; ranks must agree (appended in 0.3.1) */
+  int reserved[16];     /* zero; room for later fields, so the struct keeps this size from 0.4 on
+                           (init and setup refuse a config whose reserved words are not zero) */
 } mccsCommConfig;
 
 void mccsCommConfigDefault(mccsCommConfig *cfg);
 /* sizeof(mccsCommConfig) as this library was built (see the ABI note above). */
 size_t mccsCommConfigSize(void);
+/* mccsCommConfigDefault for a caller that states its struct size: writes
+ * nothing and returns mccsInvalidArgument unless `size` is this library's
+ * sizeof(mccsCommConfig), so a caller built against another header can never
+ * have bytes written past its struct. */
+mccsResult_t mccsCommConfigDefaultSized(mccsCommConfig *cfg, size_t size);
 
 /* One process drives `nranks` ranks (the reference service model: one mccs
  * process owns every GPU of the host).  devices[r] is rank r's GPU; devices
@@ -206,6 +216,22 @@ int mccsCommLastAlgo(mccsComm_t comm);
  * atomics).  Otherwise every AllReduce takes the ring, except buckets up to
  * ll_bytes, whose LL one-shot makes no remote atomics. */
 int mccsCommDirectEnabled(mccsComm_t comm);
+/* Node gate (connect-time self-test, run when a communicator spans two or
+ * more GPUs; MCCS_GATE=0 skips it, MCCS_GATE=1 forces it): one exact-sum
+ * AllReduce through the ring in its configured hand-off and through each
+ * enabled direct variant, with every rank agreeing on the verdicts.  A wrong
+ * ring sum steps every rank down uncached -> uncached + release -> cached
+ * (system-scope fences); a wrong direct sum disables that variant.
+ * info4[0] 1 if the gate ran, [1] the hand-off the comm now runs (MCCS_FIFO_*),
+ * [2] MCCS_GATE_* bits that failed, [3] MCCS_GATE_* direct variants disabled. */
+#define MCCS_GATE_RING_UNCACHED 0x1 /* ring, relaxed hand-off on uncached FIFOs */
+#define MCCS_GATE_RING_RELEASE 0x2  /* ring, release fence before each post */
+#define MCCS_GATE_RING_SYSTEM 0x4   /* ring, system-scope release/acquire (reference) */
+#define MCCS_GATE_LL 0x8            /* LL one-shot */
+#define MCCS_GATE_ONESHOT 0x10      /* one-shot */
+#define MCCS_GATE_TWOSHOT 0x20      /* two-shot */
+#define MCCS_GATE_NO_ATOMICS 0x40   /* some rank cannot perform peer atomics (direct kernel off) */
+mccsResult_t mccsCommGateInfo(mccsComm_t comm, int *info4);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
 const char *mccsGetErrorString(mccsResult_t r);

@@ -71,7 +71,7 @@ class _CommConfig(ctypes.Structure):
                 ("block_threads", _c_int), ("locality", _c_int), ("fifo_memory", _c_int),
                 ("timeout_ms", _c_int), ("work_fifo_depth", _c_int), ("bridge_streams", _c_int),
                 ("rings", _P(_c_int)), ("fifo_slots", _c_int), ("direct_bytes", _c_int),
-                ("oneshot_bytes", _c_int), ("ll_bytes", _c_int)]
+                ("oneshot_bytes", _c_int), ("ll_bytes", _c_int), ("reserved", _c_int * 16)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/mccs_hip.h
@@ -92,6 +92,7 @@ SIGNATURES: dict[str, tuple] = {
                  _c_void_p]),
     "mccsCommConfigDefault": (None, [_P(_CommConfig)]),
     "mccsCommConfigSize": (_c_size_t, []),
+    "mccsCommConfigDefaultSized": (_c_int, [_P(_CommConfig), _c_size_t]),
     "mccsCommInitAll": (_c_int, [_P(_c_void_p), _c_int, _P(_c_int), _P(_CommConfig)]),
     "mccsConnectHandleSize": (_c_size_t, []),
     "mccsCommSetupRank": (_c_int, [_P(_c_void_p), _c_int, _c_int, _c_int, _P(_CommConfig), _c_void_p]),
@@ -109,6 +110,7 @@ SIGNATURES: dict[str, tuple] = {
     "mccsCommLastAlgo": (_c_int, [_c_void_p]),
     "mccs_ll_default": (_c_int, [_c_int]),
     "mccsCommDirectEnabled": (_c_int, [_c_void_p]),
+    "mccsCommGateInfo": (_c_int, [_c_void_p, _P(_c_int)]),
     "mccs_ring_profile": (_c_int, [_c_int, _P(ctypes.c_ulonglong), _c_int]),
     "mccsMemAllocShared": (_c_int, [_c_int, _c_size_t, _P(_c_void_p), _c_void_p]),
     "mccsMemFreeShared": (_c_int, [_c_int, _c_void_p]),

@@ -89,8 +89,10 @@ class CommConfig:
         c = _CommConfig()
         _lib.load().mccsCommConfigDefault(ctypes.byref(c))
         for f, _ in _CommConfig._fields_:
+            if f in ("rings", "reserved"):
+                continue
             v = getattr(self, f)
-            if f != "rings" and v is not None:
+            if v is not None:
                 setattr(c, f, int(v))
         keep = None
         if self.rings is not None:
@@ -137,6 +139,14 @@ class Communicator:
     @property
     def handle(self) -> int:
         return self._h.value
+
+    def gate_info(self) -> dict:
+        """Outcome of the node gate (mccsCommGateInfo): whether it ran, the
+        hand-off the comm now runs (MCCS_FIFO_*), the MCCS_GATE_* bits that
+        failed and the direct variants it disabled."""
+        info = (ctypes.c_int * 4)()
+        _lib.check(_sig().mccsCommGateInfo(self._h, info), "mccsCommGateInfo")
+        return {"ran": bool(info[0]), "fifo_mode": info[1], "failed": info[2], "disabled": info[3]}
 
     def rings(self) -> list[list[int]]:
         out = []

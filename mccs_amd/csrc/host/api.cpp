@@ -8,6 +8,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -103,6 +104,8 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   mccsCommConfig cfg;
   mccsCommConfigDefault(&cfg);
   if (user_cfg) cfg = *user_cfg;
+  for (int w : cfg.reserved)
+    if (w != 0) return mccsInvalidArgument;  // a field this library does not know
   fill_defaults(&cfg, nranks);
   MCCS_CHECK(validate_cfg(cfg, nranks));
   if (rank < 0 || rank >= nranks) return mccsInvalidArgument;
@@ -131,6 +134,7 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   }
   c->cfg.rings = nullptr;  // not owned
   c->nch = (int)c->rings.size();
+  if (const char* v = std::getenv("MCCS_SLICE_STEPS")) c->slice_steps = std::atoi(v) == 2 ? 2 : ALLREDUCE_CHUNKSTEPS;
   c->block_threads = cfg.block_threads;
   // auto lanes: ~64 streaming workgroups per rank (128 at n = 2).  A lane's
   // throughput is bound by its per-slice latency chain (flag poll, loads,
@@ -267,6 +271,13 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
       cs[i]->direct_ok = atomics;
     }
     for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_build_device(cs[i]);
+    // node gate: one process sees every rank, so the host combines their verdicts
+    bool distinct = false;
+    for (int i = 1; i < nranks; ++i) distinct = distinct || devices[i] != devices[0];
+    if (r == mccsSuccess && nranks > 1 && gate_wanted(distinct)) {
+      std::vector<bool> atomics_ok(nranks, atomics);
+      r = comm_gate(cs, atomics_ok);
+    }
   }
   if (r != mccsSuccess) {
     for (auto c : cs)
@@ -278,6 +289,12 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
   }
   for (int i = 0; i < nranks; ++i) comms[i] = (mccsComm_t)cs[i];
   return mccsSuccess;
+}
+
+// Two connect handles name the same GPU: same host and PCI bus id (ordinals
+// are local to a process, so they would match across different GPUs).
+static bool same_gpu(const ConnectHandle& a, const ConnectHandle& b) {
+  return std::strncmp(a.host, b.host, sizeof(a.host)) == 0 && std::strncmp(a.pci, b.pci, sizeof(a.pci)) == 0;
 }
 
 extern "C" size_t mccsConnectHandleSize(void) { return sizeof(ConnectHandle); }
@@ -323,6 +340,16 @@ extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks,
   h.ring_cap = coresident_ring_blocks(c->block_threads, device);
   h.arena_bytes = c->layout.total();
   h.buffer_size = c->layout.buffer_size;
+  h.direct_bytes = c->cfg.direct_bytes;
+  h.oneshot_bytes = c->cfg.oneshot_bytes;
+  h.ll_bytes = c->cfg.ll_bytes;
+  h.fifo_slots = c->cfg.fifo_slots;
+  h.slice_steps = c->slice_steps;
+  h.block_threads = c->block_threads;
+  if (hipDeviceGetPCIBusId(h.pci, sizeof(h.pci) - 1, device) != hipSuccess) {
+    (void)hipGetLastError();
+    std::snprintf(h.pci, sizeof(h.pci), "ordinal:%d", device);
+  }
   gethostname(h.host, sizeof(h.host) - 1);
   std::memcpy(handle_out, &h, sizeof(h));
   *out = (mccsComm_t)c;
@@ -339,6 +366,12 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
     if (h.magic != kHandleMagic || h.rank != r || h.nranks != c->nranks || h.nch != c->nch ||
         h.arena_bytes != c->layout.total() || h.buffer_size != c->layout.buffer_size)
       return mccsInvalidArgument;  // ranks disagree on the communicator profile
+    // ... or on which kernel / slice shape a call takes (both ends of every
+    // connection must run the same one: ADVICE r03)
+    if (h.direct_bytes != c->cfg.direct_bytes || h.oneshot_bytes != c->cfg.oneshot_bytes ||
+        h.ll_bytes != c->cfg.ll_bytes || h.fifo_slots != c->cfg.fifo_slots || h.slice_steps != c->slice_steps ||
+        h.block_threads != c->block_threads)
+      return mccsInvalidArgument;
     all_uc = all_uc && h.fifo_memory != MCCS_FIFO_DEVICE;
     release = release || h.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
     if (h.lanes != hs[0].lanes || h.lanes_auto != hs[0].lanes_auto) return mccsInvalidArgument;
@@ -355,8 +388,7 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
     int max_share = 1, cap = 1 << 30;
     for (int r = 0; r < c->nranks; ++r) {
       int share = 0;
-      for (int q = 0; q < c->nranks; ++q)
-        share += hs[q].device == hs[r].device && std::strncmp(hs[q].host, hs[r].host, sizeof(hs[q].host)) == 0;
+      for (int q = 0; q < c->nranks; ++q) share += same_gpu(hs[q], hs[r]);
       max_share = std::max(max_share, share);
       if (hs[r].ring_cap > 0) cap = std::min(cap, (int)hs[r].ring_cap);
     }
@@ -376,7 +408,9 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
     if (r == c->rank) continue;
     const ConnectHandle& h = hs[r];
     if (h.pid == (int32_t)getpid()) return mccsInvalidUsage;  // same process: use mccsCommInitAll
-    (void)enable_peer(c->device, h.device);                    // best effort; IPC maps regardless
+    int peer_dev = -1;                                         // the peer's GPU as this process numbers it
+    if (hipDeviceGetByPCIBusId(&peer_dev, h.pci) != hipSuccess) (void)hipGetLastError();
+    if (peer_dev >= 0) (void)enable_peer(c->device, peer_dev);  // best effort; IPC maps regardless
     void* p = nullptr;
     hipError_t e = hipIpcOpenMemHandle(&p, h.ipc, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) {
@@ -388,12 +422,38 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
   }
   c->all_uncached = all_uc;
   c->fifo_release = release;
-  {
-    std::vector<int> devs;
-    for (int r = 0; r < c->nranks; ++r) devs.push_back(hs[r].device);
-    c->direct_ok = devices_p2p_atomics(devs);
+  // Peer atomics as THIS process sees them: every peer's GPU looked up by PCI
+  // bus id (ordinals are per process).  A peer GPU this process cannot see,
+  // or cannot do atomics on, turns the count-based direct variants off here;
+  // the node gate's vote then turns them off on every rank alike.
+  bool atomics = true, distinct = false;
+  for (int r = 0; r < c->nranks; ++r) {
+    if (same_gpu(hs[r], hs[c->rank])) continue;
+    distinct = true;
+    int dev = -1, ok = 0;
+    if (hipDeviceGetByPCIBusId(&dev, hs[r].pci) != hipSuccess || dev < 0) {
+      (void)hipGetLastError();
+      atomics = false;
+    } else if (rt().P2PAtomics(&ok, c->device, dev) != hipSuccess || !ok) {
+      (void)hipGetLastError();
+      atomics = false;
+    }
   }
-  return comm_build_device(c);
+  c->direct_ok = atomics;
+  MCCS_CHECK(comm_build_device(c));
+  if (gate_wanted(distinct)) {
+    std::vector<Comm*> cs{c};
+    mccsResult_t r = comm_gate(cs, std::vector<bool>{atomics});
+    if (r != mccsSuccess) {
+      c->connected = false;  // the caller destroys it; no collective may run on it
+      return r;
+    }
+  } else if (distinct) {
+    // no gate, no vote: keep the count-based direct variants only where every
+    // rank can be trusted to decide alike (they cannot tell without a vote)
+    c->direct_ok = false;
+  }
+  return mccsSuccess;
 }
 
 extern "C" mccsResult_t mccsAllReduce(const void* sendbuff, void* recvbuff, size_t count, int dtype, int op,
@@ -473,7 +533,10 @@ extern "C" mccsResult_t mccsCommInfo(mccsComm_t comm, int* info) {
   info[3] = c->nch;
   info[4] = c->lanes;
   info[5] = c->block_threads;
-  info[6] = !c->all_uncached ? MCCS_FIFO_DEVICE : c->fifo_release ? MCCS_FIFO_UNCACHED_RELEASE : MCCS_FIFO_UNCACHED;
+  // the hand-off the launches run (after any node-gate step-down)
+  info[6] = c->kcfg.fence_mode == MCCS_FENCE_SYSTEM             ? MCCS_FIFO_DEVICE
+            : c->kcfg.fence_mode == MCCS_FENCE_UNCACHED_RELEASE ? MCCS_FIFO_UNCACHED_RELEASE
+                                                                : MCCS_FIFO_UNCACHED;
   return mccsSuccess;
 }
 

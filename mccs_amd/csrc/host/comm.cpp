@@ -117,15 +117,19 @@ bool devices_p2p_atomics(const std::vector<int>& devices) {
 mccsResult_t comm_set_kernel_cfg(Comm* c) {
   mccsRingKernelCfg k{};
   k.fence_mode = !c->all_uncached ? MCCS_FENCE_SYSTEM : c->fifo_release ? MCCS_FENCE_UNCACHED_RELEASE : MCCS_FENCE_UNCACHED;
+  // the node gate only ever steps the hand-off down (gate.cpp)
+  if (c->gate_fence == MCCS_FENCE_SYSTEM) k.fence_mode = MCCS_FENCE_SYSTEM;
+  else if (c->gate_fence == MCCS_FENCE_UNCACHED_RELEASE && k.fence_mode == MCCS_FENCE_UNCACHED)
+    k.fence_mode = MCCS_FENCE_UNCACHED_RELEASE;
   k.err_line = 1;  // d_abort is a 64-byte line of ours: errors go to its word 1
   k.fifo_slots = (uint32_t)c->cfg.fifo_slots;
   const int tmo = c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms;
   k.timeout_ticks = tmo < 0 ? 0 : (uint64_t)tmo * 100000ull;  // s_memrealtime: 100 MHz
   // one 4-step slice per chunk (2 slices in flight per lane): one flag
   // round trip and one drain per chunk instead of two; +6-27 % on the virtual
-  // node.  MCCS_SLICE_STEPS=2 restores the reference's SliceSteps.
-  k.slice_steps = ALLREDUCE_CHUNKSTEPS;
-  if (const char* v = std::getenv("MCCS_SLICE_STEPS")) k.slice_steps = std::atoi(v) == 2 ? 2 : 4;
+  // node.  MCCS_SLICE_STEPS=2 restores the reference's SliceSteps (read at
+  // communicator creation, carried in the connect handle: both ends agree).
+  k.slice_steps = (uint32_t)c->slice_steps;
   if (const char* v = std::getenv("MCCS_RING_PROFILE")) k.profile = std::atoi(v) != 0;
   c->kcfg = k;  // travels in every launch's arguments (no device global)
   return mccsSuccess;

@@ -98,6 +98,15 @@ struct ConnectHandle {
   uint64_t buffer_size;
   hipIpcMemHandle_t ipc;
   char host[64];
+  // Everything both ends of a connection must agree on beyond the arena size
+  // (thresholds that round to the same arena let ranks pick
+  // different kernels for one call): the resolved direct thresholds, the FIFO
+  // depth and the slice size.  Connect refuses any mismatch.
+  int32_t direct_bytes, oneshot_bytes, ll_bytes;
+  int32_t fifo_slots, slice_steps, block_threads;
+  // PCI bus id of the rank's GPU: device ordinals are local to a process
+  // (HIP_VISIBLE_DEVICES), so co-location and peer lookups use this
+  char pci[32];
 };
 constexpr uint32_t kHandleMagic = 0x6d636373;  // "mccs"
 
@@ -189,6 +198,13 @@ struct Comm {
   // derive it from the same device set, so they agree.
   bool direct_ok = false;
   int last_algo = -1;    // MCCS_ALGO_* of the latest launch
+  int slice_steps = ALLREDUCE_CHUNKSTEPS;  // FIFO steps per ring slice (MCCS_SLICE_STEPS=2: the reference's 2)
+  // node gate (gate.cpp): a hand-off mode the gate stepped down to (-1: none;
+  // MCCS_FENCE_UNCACHED_RELEASE or MCCS_FENCE_SYSTEM), whether it ran, the
+  // MCCS_GATE_* bits that failed and the direct variants it disabled
+  int gate_fence = -1;
+  bool gate_ran = false;
+  unsigned gate_failed = 0, gate_disabled = 0;
 };
 
 // comm.cpp
@@ -203,6 +219,9 @@ mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream
 mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one
 int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live library comm's device struct, else 0
 void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
+// gate.cpp
+bool gate_wanted(bool distinct_gpus);
+mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_ok);
 // plan.cpp
 void plan_discard(Comm* c);  // drops the pending plan
 mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count);

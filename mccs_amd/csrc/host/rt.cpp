@@ -251,6 +251,7 @@ class FakeRuntime final : public DeviceRuntime {
         const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
         for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(ma->comm[k]) == cur_;
         inl = ma->inline_works;
+        extra = " fence=" + std::to_string(ma->cfg.fence_mode);
       }
     }
     note("launch dev=" + std::to_string(cur_) + " grid=" + std::to_string(grid.x) + "x" + std::to_string(grid.y) +

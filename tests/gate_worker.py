@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""The node gate across processes (a worker of tests/test_gpu_gate.py).
+
+  python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29541 tests/gate_worker.py
+
+One rank per process, all on cuda:0 of the one-GPU box, MCCS_GATE=1 (the
+gate runs although no pair of ranks is on distinct GPUs).  Cases, each on a
+fresh communicator:
+  clean      nothing injected: the gate passes every path, the comm keeps the
+             relaxed uncached hand-off and every default path;
+  ring       rank 1 alone reports a wrong ring sum (MCCS_GATE_INJECT): the
+             ring vote carries it to every rank, all step down to the
+             release mode together;
+  oneshot    rank 0 alone reports a wrong one-shot sum: every rank disables
+             the one-shot, its buckets take the ring on every rank;
+  mismatch   ranks resolve different one-shot thresholds that round to the
+             same arena: Connect refuses on every rank.
+After each connect, exact-sum AllReduces at LL / one-shot / ring sizes check
+the results and which kernel ran.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+G_RING_UC, G_ONE = 0x1, 0x10
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    from mccs_amd import comm as C
+    from mccs_amd import refdrive
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def exchange(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+
+    os.environ["MCCS_GATE"] = "1"
+    os.environ["MCCS_TEST_HOOKS"] = "1"
+    cases = {"clean": {}, "ring": {"MCCS_GATE_INJECT": hex(G_RING_UC), "MCCS_GATE_INJECT_RANK": "1"},
+             "oneshot": {"MCCS_GATE_INJECT": hex(G_ONE), "MCCS_GATE_INJECT_RANK": "0"},
+             "mismatch": {"MCCS_ONESHOT_BYTES": "1000000" if rank == 0 else "1048576"}}
+    results = {}
+    dv = torch.device("cuda", dev)
+    for name, env in cases.items():
+        for k in ("MCCS_GATE_INJECT", "MCCS_GATE_INJECT_RANK", "MCCS_ONESHOT_BYTES"):
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        dist.barrier()
+        try:
+            comm = C.init_communicator_rank(rank, world, dev, exchange, C.CommConfig(timeout_ms=20000))
+        except RuntimeError as e:
+            results[f"{name}/connect"] = {"ok": name == "mismatch" and "mccsCommConnect" in str(e), "err": str(e)[:200]}
+            continue
+        if name == "mismatch":
+            results["mismatch/connect"] = {"ok": False, "err": "connected"}
+            comm.destroy()
+            continue
+        gi = comm.gate_info()
+        want_mode = 2 if name == "ring" else 0  # MCCS_FIFO_UNCACHED_RELEASE / MCCS_FIFO_UNCACHED
+        ok = gi["ran"] and gi["fifo_mode"] == want_mode and comm.fifo_memory == want_mode
+        ok = ok and gi["disabled"] == (G_ONE if name == "oneshot" else 0)
+        ok = ok and (gi["failed"] & G_RING_UC) == (G_RING_UC if name == "ring" else 0)
+        results[f"{name}/gate"] = {"ok": bool(ok), "info": gi}
+        # LL-sized, one-shot-sized and ring-sized buckets (defaults at n = 2:
+        # LL <= 128 KiB, one-shot <= 2 MiB, two-shot off)
+        for nbytes, algo in ((32 << 10, "ll"), (512 << 10, "ring" if name == "oneshot" else "oneshot"),
+                             (8 << 20, "ring")):
+            count = nbytes // 4
+            send = refdrive.exact_inputs(torch, count, rank, torch.float32, dv)
+            want = refdrive.expected_exact(torch, count, world, torch.float32, dv)
+            recv = torch.empty_like(send)
+            C.all_reduce(comm, send, recv, count, 7, 0)
+            comm.sync()
+            results[f"{name}/{nbytes}"] = {"ok": bool(torch.equal(recv, want)) and comm.last_algo() == algo,
+                                           "algo": comm.last_algo()}
+        comm.destroy()
+    allres = [None] * world
+    dist.all_gather_object(allres, results)
+    if rank == 0:
+        merged = {k: all(r[k]["ok"] for r in allres) for k in results}
+        print(json.dumps({"world": world, "cases": merged, "all_ok": all(merged.values()),
+                          "detail": {k: [r[k] for r in allres] for k in results if not merged[k]}}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -69,11 +69,11 @@ def test_requested_channel_count():
 def test_config_struct_matches_header():
     from mccs_amd._lib import _CommConfig
 
-    # 9 ints, pad, pointer, fifo_slots, direct_bytes, oneshot_bytes, ll_bytes
-    assert ctypes.sizeof(_CommConfig) == 9 * 4 + 4 + 8 + 4 * 4
+    # 9 ints, pad, pointer, fifo_slots, direct_bytes, oneshot_bytes, ll_bytes, 16 reserved words
+    assert ctypes.sizeof(_CommConfig) == 9 * 4 + 4 + 8 + 4 * 4 + 16 * 4
     assert _CommConfig.fifo_slots.offset == 48
     assert _CommConfig.direct_bytes.offset == 52 and _CommConfig.oneshot_bytes.offset == 56
-    assert _CommConfig.ll_bytes.offset == 60
+    assert _CommConfig.ll_bytes.offset == 60 and _CommConfig.reserved.offset == 64
     assert comm._sig().mccsCommConfigSize() == ctypes.sizeof(_CommConfig)
     lib = comm._sig()
     c = _CommConfig()
