@@ -9,8 +9,9 @@
   extern "C" __global__ void __launch_bounds__(MCCS_RING_MAX_THREADS)                                  \
       mccsKernel_AllReduce_RING_SIMPLE_##OPN##_##TN(mccsDevComm* comm, uint64_t channelMask,           \
                                                     mccsDevWork* workHead) {                           \
-    mccs::ring_kernel_body<mccsFuncAllReduce, DT, OPV>(comm, channelMask, workHead, blockIdx.x, gridDim.x, \
-                                                       mccs::kRefCfg);                                 \
+    mccs::ring_kernel_body<mccsFuncAllReduce, DT, OPV, mccs::kRefUnroll<DT>>(comm, channelMask, workHead,  \
+                                                                             blockIdx.x, gridDim.x,       \
+                                                                             mccs::kRefCfg);              \
   }
 
 #define MCCS_AR_CASE(OPN, OPV, TN, DT)                                                                       \

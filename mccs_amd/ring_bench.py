@@ -569,6 +569,15 @@ def cpu_ring_baseline(world: int, nbytes: int, nchannels: int, budget_s: float =
                                       f"ring (same schedule and FIFO protocol), {reps} AllReduces in {el:.2f}s"}
 
 
+# The ring's only counter-measured traffic: the n = 2 virtual node (one GPU,
+# rocprofv3 FETCH_SIZE / WRITE_SIZE with the gfx950 corrections), carried in
+# the N > 1 line under its own name so nobody reads it as a node measurement.
+VNODE_N2_TRAFFIC = {"traffic_over_algorithmic": 1.0043, "where": "n = 2 virtual node (both ranks on one MI355X), "
+                    "128 MiB fp32, rocprofv3 PMC", "source": "profiles/r03_ring_vnode_summary.json pmc_n2"}
+TRAFFIC_NOT_MEASURED = ("not measured on the node: the PMC passes run on the 1-GPU box only (no 8-GPU box is "
+                        "available to this repo's runs); see traffic_virtual_node_n2 for the one measured ratio")
+
+
 def ring_roofline(world, nbytes, per_step_s, links, ranks_share_gpu, kernel):
     """Bound of one rank's ring AllReduce.  On a node: the xGMI links the rank
     sends on, per-rank link bytes 2(n-1)/n*S.  When every rank shares one
@@ -579,13 +588,15 @@ def ring_roofline(world, nbytes, per_step_s, links, ranks_share_gpu, kernel):
         hbm = (6 * world - 4) * nbytes
         ach = hbm / per_step_s / 1e9
         return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": kernel,
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "traffic_note": TRAFFIC_NOT_MEASURED,
+                "traffic_virtual_node_n2": VNODE_N2_TRAFFIC, "kernel": kernel,
                 "note": f"ranks share one GPU: (6n-4)*S = {hbm} algorithmic HBM bytes per AllReduce, all n ranks"}
     link_bytes = 2 * (world - 1) / world * nbytes
     ach = link_bytes / per_step_s / 1e9
     peak = links * XGMI_LINK_GBPS_PER_DIR
     return {"bound": "xgmi", "achieved": round(ach, 2), "peak": peak, "unit": "GB/s", "frac": round(ach / peak, 4),
-            "traffic": None, "kernel": kernel,
+            "traffic": None, "traffic_note": TRAFFIC_NOT_MEASURED, "traffic_virtual_node_n2": VNODE_N2_TRAFFIC,
+            "kernel": kernel,
             "note": f"per-rank link bytes 2(n-1)/n*S over {links} distinct outgoing links x "
                     f"{XGMI_LINK_GBPS_PER_DIR} GB/s per direction (spec)"}
 
@@ -920,7 +931,8 @@ def setup2_roofline(jobs, ranks_share_gpu: bool) -> dict:
     if ranks_share_gpu:
         peak = HBM_PEAK_GBPS
     return {"bound": "hbm" if ranks_share_gpu else "xgmi", "achieved": round(ach, 2), "peak": round(peak, 2),
-            "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None,
+            "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None, "traffic_note": TRAFFIC_NOT_MEASURED,
+            "traffic_virtual_node_n2": VNODE_N2_TRAFFIC,
             "kernel": "ring_multi_kernel<AllReduce, half, Sum>", "per_job": per,
             "note": ("ranks share one GPU: all jobs' (6n-4)*S algorithmic HBM bytes per call" if ranks_share_gpu
                      else "per job: per-rank link bytes 2(n-1)/n*S per call over its distinct outgoing links x "

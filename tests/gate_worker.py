@@ -54,7 +54,8 @@ def main():
     results = {}
     dv = torch.device("cuda", dev)
     for name, env in cases.items():
-        for k in ("MCCS_GATE_INJECT", "MCCS_GATE_INJECT_RANK", "MCCS_ONESHOT_BYTES"):
+        for k in ("MCCS_GATE_INJECT", "MCCS_GATE_INJECT_RANK", "MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES",
+                  "MCCS_LL_BYTES"):
             os.environ.pop(k, None)
         os.environ.update(env)
         dist.barrier()

@@ -17,6 +17,7 @@ import sys
 import pytest
 
 pytestmark = pytest.mark.gpu
+DIRECT_DEFAULTS = True  # the gate tests the library defaults (conftest otherwise pins the ring)
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
