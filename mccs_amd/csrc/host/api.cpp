@@ -490,9 +490,9 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
   if (!c) return mccsInvalidArgument;
   DeviceGuard g(c->device);
   // the latest launch recorded the comm event only if something consumes it
-  // (plan.cpp); otherwise wait for every stream of the device, a superset
-  if (c->event_recorded) MCCS_HIP(rt().EventSynchronize(c->event));
-  else MCCS_HIP(rt().DeviceSynchronize());
+  // (plan.cpp); else the event of the comm it was fused with; else wait for
+  // every stream of the device, a superset
+  MCCS_HIP(comm_wait_last_launch(c));
   if (c->stream) MCCS_HIP(rt().StreamSynchronize(c->stream));
   // the communicator's abort line: word 0 abortFlag, word 1 the error bits its
   // kernels reported (ring_cfg.h), so another communicator's failure never

@@ -17,6 +17,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <set>
 #include <mutex>
 
 #include "comm.h"
@@ -182,6 +183,7 @@ void comm_pool_drop_generation(unsigned generation) {
 // reference's 8 slots) can refuse a library communicator built with another.
 static std::mutex g_live_mu;
 static std::map<const void*, int> g_live_fifo_slots;
+static std::set<Comm*> g_live_comms;  // connected comms of this process (Comm::sync_owner lookups)
 
 int comm_fifo_slots_of(const void* d_comm) {
   std::lock_guard<std::mutex> lk(g_live_mu);
@@ -346,6 +348,7 @@ mccsResult_t comm_build_device(Comm* c) {
   {
     std::lock_guard<std::mutex> lk(g_live_mu);
     g_live_fifo_slots[c->d_comm] = c->cfg.fifo_slots;
+    g_live_comms.insert(c);
   }
   c->connected = true;
   return mccsSuccess;
@@ -377,15 +380,30 @@ mccsResult_t comm_make_event_ipc(Comm* c) {
   return mccsSuccess;
 }
 
+hipError_t comm_wait_last_launch(Comm* c) {
+  if (c->event_recorded) return rt().EventSynchronize(c->event);
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    if (c->sync_event && c->sync_owner && g_live_comms.count(const_cast<Comm*>(c->sync_owner)))
+      return rt().EventSynchronize(c->sync_event);
+  }
+  return rt().DeviceSynchronize();  // nothing recorded the launch: every stream of the device
+}
+
 mccsResult_t comm_free(Comm* c) {
   DeviceGuard g(c->device);
+  // the last launch (any stream) must be done before its arenas are reused
+  (void)comm_wait_last_launch(c);
   {
     std::lock_guard<std::mutex> lk(g_live_mu);
     g_live_fifo_slots.erase(c->d_comm);
+    g_live_comms.erase(c);
+    for (Comm* x : g_live_comms)
+      if (x->sync_owner == c) {
+        x->sync_owner = nullptr;
+        x->sync_event = nullptr;
+      }
   }
-  // the last launch (any stream) must be done before its arenas are reused
-  if (c->event_recorded) (void)rt().EventSynchronize(c->event);
-  else (void)rt().DeviceSynchronize();
   if (c->stream) (void)rt().StreamSynchronize(c->stream);
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
     if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)hipIpcCloseMemHandle(c->peer_arena[r]);

@@ -176,6 +176,13 @@ struct Comm {
   // at ~5 us of device time per call (2 processes, 32 KiB fp16: 16.5 vs
   // 11.6 us per AllReduce).  Without it mccsCommSync waits for the device.
   bool event_recorded = false;
+  // When the latest launch did not record `event` but was fused with a comm
+  // whose event it did record (rank slots k >= 1 of a fused launch): that
+  // event, so mccsCommSync waits on this launch and not on the whole device
+  // (a device-wide wait would also wait on other communicators' kernels that
+  // spin on their peers: ADVICE r03).  Cleared when the owner is freed.
+  hipEvent_t sync_event = nullptr;
+  const Comm* sync_owner = nullptr;
   hipEvent_t user_event = nullptr;  // user -> comm
   bool connected = false;
   bool failed = false;
@@ -214,6 +221,7 @@ mccsResult_t comm_switch_to_device_arena(Comm* c);
 mccsResult_t comm_build_device(Comm* c);
 void default_rings(int nranks, int nch_req, std::vector<std::vector<int>>* rings);
 mccsResult_t comm_free(Comm* c);
+hipError_t comm_wait_last_launch(Comm* c);  // host wait for the comm's latest launch
 mccsResult_t comm_set_kernel_cfg(Comm* c);
 mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream on first use
 mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one

@@ -316,11 +316,19 @@ class RefDrivenRank:
             local_err = e
         names = allgather("" if local_err else name)
         self.base = [0] * n
+        # only the ring neighbours' segments are touched (each channel's prev
+        # and next): an 8-rank, 32-channel rank maps 2 of 7 peers' 128 MiB
+        neigh = set()
+        for ring in self.rings:
+            pos = ring.index(rank)
+            neigh.update((ring[(pos + 1) % n], ring[(pos - 1) % n]))
         if not local_err and all(names):
             try:
                 for r in range(n):
                     if r == rank:
                         self.base[r] = self._segs[0].dev
+                        continue
+                    if r not in neigh:
                         continue
                     seg = HostSegment(names[r], nbytes, create=False)
                     self._segs.append(seg)

@@ -276,7 +276,8 @@ def test_comm_events_ride_on_the_launch(fake, monkeypatch):
 def test_fused_ranks_record_their_events_only_when_consumed(fake):
     """Ranks sharing a device run as one launch: the first comm's event rides
     on it; the others' events are recorded only when consumed (here: not), and
-    their mccsCommSync waits on the device instead."""
+    their mccsCommSync waits on the launching comm's event (not the device:
+    ADVICE r03)."""
     fake(4)
     comms = C.init_all([0, 0, 1, 1, 2, 2, 3, 3], C.CommConfig(buffer_size=1 << 20, lanes=2, channel_count=1,
                                                               rings=[[0, 1, 2, 3, 4, 5, 6, 7]]))
@@ -289,7 +290,7 @@ def test_fused_ranks_record_their_events_only_when_consumed(fake):
         for c in comms:
             c.sync()
         waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
-        assert waits.count("event") == 4 and waits.count("device") == 4, waits
+        assert waits.count("event") == 8 and waits.count("device") == 0, waits
     finally:
         for c in comms:
             c.destroy()
@@ -547,4 +548,34 @@ def test_ll_runs_without_peer_atomics(fake, monkeypatch):
             c.sync()
     finally:
         for c in comms:
+            c.destroy()
+
+
+def test_fused_rank_sync_waits_on_the_launch_not_the_device(fake):
+    """Rank slots k >= 1 of a fused launch record no event of their own; their
+    mccsCommSync waits on the launching comm's stop event instead of the whole
+    device, which would also wait on other communicators' spinning kernels
+    (ADVICE r03).  Destroying the launching comm first falls back safely (to
+    the rank's own event or the device, never the freed event)."""
+    fake(2)
+    comms = C.init_all([0, 0, 1, 1], C.CommConfig(buffer_size=1 << 20, lanes=1))
+    try:
+        _log()
+        _allreduce_group(comms)
+        _log()
+        for c in comms:
+            c.sync()
+        waits = [kv for k, kv in _log() if k == "host_wait"]
+        assert waits and all(kv["what"] in ("event", "memcpy") for kv in waits), waits
+        # the launching comm of each device goes first: its fused peer falls back to a device wait
+        _allreduce_group(comms)
+        comms[0].destroy()
+        comms[2].destroy()
+        _log()
+        comms[1].sync()
+        waits = [kv for k, kv in _log() if k == "host_wait"]
+        # never a wait on the destroyed comm's event (the fake reports such an event's device as -1)
+        assert waits and all(kv["dev"] != "-1" for kv in waits), waits
+    finally:
+        for c in (comms[1], comms[3]):
             c.destroy()
