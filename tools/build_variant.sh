@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
-# Builds an A/B variant of libmccs_hip.so with extra -D flags into exp/<name>.so
-# (use it with MCCS_LIB_PATH=exp/<name>.so).  Only the ring translation units
+# Builds an A/B variant of libmccs_hip.so with extra -D flags into
+# $VARIANT_DIR/<name>.so (default abvar/: git-ignored, but it travels to the
+# GPU box; use it with MCCS_LIB_PATH=abvar/<name>.so).  Only the ring translation units
 # (ring.hip, ring_ar_*.hip) are recompiled, in parallel; VARIANT_SRCS=reduce
 # recompiles reduce.hip instead.
 #   tools/build_variant.sh <name> -DMCCS_RING_INPUT_NT=1 ...
@@ -8,16 +9,17 @@
 set -eu
 R=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
-mkdir -p "$R/exp/$name"
+OUT="$R/${VARIANT_DIR:-abvar}"
+mkdir -p "$OUT/$name"
 pids=()
 pat=${VARIANT_SRCS:-ring}
 for src in "$R"/mccs_amd/csrc/$pat*.hip; do
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -I"$R/mccs_amd/csrc" "$@" \
-    -c -x hip "$src" -o "$R/exp/$name/$(basename "$src").o" &
+    -c -x hip "$src" -o "$OUT/$name/$(basename "$src").o" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
 objs=$(ls "$R"/build/obj/*.o | grep -v "/$pat[^/]*\.hip\.o\$")
-hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/exp/$name.so" "$R"/exp/$name/*.o $objs -lpthread
-rm -rf "$R/exp/$name"
-echo "$R/exp/$name.so"
+hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/$name.so" "$OUT"/$name/*.o $objs -lpthread
+rm -rf "$OUT/$name"
+echo "$OUT/$name.so"
