@@ -736,6 +736,15 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
         extras["allgather_16MiB_per_rank"] = extra_allgather(torch, dist, C, comm, rank, world, dev)
         extras["size_sweep_fp16"] = size_sweep(torch, dist, C, comm, rank, world, dev)
     info = {"channels": comm.nchannels, "lanes": comm.lanes, "block_threads": comm.block_threads}
+    # the connect-time node gate of the timed communicator (csrc/host/gate.cpp):
+    # whether it ran, the hand-off it left (MCCS_FIFO_* code: what the line
+    # really ran), the paths it found wrong and the direct variants it disabled
+    gi = comm.gate_info()
+    extras["node_gate"] = {"ran": gi["ran"], "fifo_memory_run": gi["fifo_mode"], "failed_bits": gi["failed"],
+                           "disabled_bits": gi["disabled"],
+                           "bits": "0x1 ring uncached, 0x2 ring release, 0x4 ring system, 0x8 LL, 0x10 one-shot, "
+                                   "0x20 two-shot, 0x40 no peer atomics",
+                           "fifo_memory_codes": "0 uncached (relaxed), 1 cached + system fences, 2 uncached + release"}
     if not getattr(args, "no_extra", False) and "size_sweep_fp16" in extras and 2 <= world <= 8:
         extras["direct_sweep_fp16"] = direct_sweep(torch, dist, C, rank, world, device, dev, exchange,
                                                    mode_config(C, mode, info), extras["size_sweep_fp16"])
