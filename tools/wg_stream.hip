@@ -45,8 +45,9 @@ using namespace mccs;
 
 constexpr int kBlock = 544;
 
-// design: 0 reg, 1 regpp, 2 lds
-template <int DES, int U, int S, int NS, int ND>
+// design: 0 reg, 1 regpp, 2 lds.  NTM: nt mask of the loads (bit 0 source 0,
+// bit 1 source 1); P0 / P1: store policy of destination 0 / 1 (reduce_copy.h)
+template <int DES, int U, int S, int NS, int ND, int NTM = 1, int P0 = kNonTemporal, int P1 = kPlain>
 __global__ void __launch_bounds__(576) stream_kernel(const float* s0, const float* s1, float* d0, float* d1,
                                                      long per_wg, long slice) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -64,15 +65,12 @@ __global__ void __launch_bounds__(576) stream_kernel(const float* s0, const floa
     float* y = d1 + base + off;
     if (data) {
       if constexpr (DES == 0) {
-        reduce_copy_rows<mccsFloat32, OpSum, U, NS, ND, 1, kNonTemporal, kPlain>(a, b, x, y, n, threadIdx.x, ndthr,
-                                                                                  false, none);
+        reduce_copy_rows<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr, false, none);
       } else if constexpr (DES == 1) {
-        reduce_copy_rows_pp<mccsFloat32, OpSum, U, NS, ND, 1, kNonTemporal, kPlain>(a, b, x, y, n, threadIdx.x,
-                                                                                     ndthr);
+        reduce_copy_rows_pp<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr);
       } else {
         const uint32_t lds = (uint32_t)(uintptr_t)smem + (uint32_t)(wave * S * NS * U * 1024);
-        lds_stream_rows<mccsFloat32, OpSum, U, S, NS, ND, 1, kNonTemporal, kPlain>(a, b, x, y, n, threadIdx.x,
-                                                                                    ndthr, lds);
+        lds_stream_rows<mccsFloat32, OpSum, U, S, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr, lds);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -84,9 +82,9 @@ struct Bufs {
   float *s0, *s1, *d0, *d1;
 };
 
-template <int DES, int U, int S, int NS, int ND>
+template <int DES, int U, int S, int NS, int ND, int NTM = 1, int P0 = kNonTemporal, int P1 = kPlain>
 static void run(const char* name, const Bufs& b, int G, long per_wg, long slice, int iters) {
-  auto k = stream_kernel<DES, U, S, NS, ND>;
+  auto k = stream_kernel<DES, U, S, NS, ND, NTM, P0, P1>;
   const size_t lds = DES == 2 ? (size_t)8 * S * NS * U * 1024 : 0;
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipEvent_t e0, e1;
@@ -102,9 +100,10 @@ static void run(const char* name, const Bufs& b, int G, long per_wg, long slice,
   float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double bytes = (double)per_wg * 4 * (NS + ND);  // per workgroup per launch
-  std::printf("{\"design\": \"%s\", \"NS\": %d, \"ND\": %d, \"U\": %d, \"S\": %d, \"G\": %d, \"slice_KiB\": %ld, "
-              "\"us\": %.1f, \"GBps_per_wg\": %.1f}\n",
-              name, NS, ND, U, S, G, slice * 4 / 1024, ms * 1e3 / iters, bytes / (ms * 1e-3 / iters) / 1e9);
+  std::printf("{\"design\": \"%s\", \"NS\": %d, \"ND\": %d, \"U\": %d, \"S\": %d, \"ntmask\": %d, \"st\": [%d, %d], "
+              "\"G\": %d, \"slice_KiB\": %ld, \"us\": %.1f, \"GBps_per_wg\": %.1f}\n",
+              name, NS, ND, U, S, NTM, P0, P1, G, slice * 4 / 1024, ms * 1e3 / iters, bytes / (ms * 1e-3 / iters) / 1e9);
+  std::fflush(stdout);
   CK(hipEventDestroy(e0));
   CK(hipEventDestroy(e1));
 }
@@ -159,20 +158,27 @@ int main(int argc, char** argv) {
   std::printf("{\"check\": \"%s\"}\n", ok ? "ok" : "FAIL");
   std::fflush(stdout);
   if (!ok) return 1;
-  run<0, 8, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
-  run<0, 16, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
-  run<1, 4, 1, 2, 2>("regpp", b, G, per_wg, slice, iters);
-  run<1, 8, 1, 2, 2>("regpp", b, G, per_wg, slice, iters);
-  run<2, 4, 2, 2, 2>("lds", b, G, per_wg, slice, iters);
-  run<2, 2, 4, 2, 2>("lds", b, G, per_wg, slice, iters);
-  run<2, 2, 3, 2, 2>("lds", b, G, per_wg, slice, iters);
-  run<0, 8, 1, 2, 1>("reg", b, G, per_wg, slice, iters);
-  run<1, 8, 1, 2, 1>("regpp", b, G, per_wg, slice, iters);
-  run<2, 4, 2, 2, 1>("lds", b, G, per_wg, slice, iters);
-  run<2, 2, 4, 2, 1>("lds", b, G, per_wg, slice, iters);
-  run<0, 8, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
-  run<1, 8, 1, 1, 2>("regpp", b, G, per_wg, slice, iters);
-  run<2, 4, 3, 1, 2>("lds", b, G, per_wg, slice, iters);
-  run<2, 8, 2, 1, 2>("lds", b, G, per_wg, slice, iters);
+  const int set = argc > 5 ? std::atoi(argv[5]) : 0;
+  if (set == 0) {
+    run<0, 8, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
+    run<1, 8, 1, 2, 2>("regpp", b, G, per_wg, slice, iters);
+    run<2, 4, 2, 2, 2>("lds", b, G, per_wg, slice, iters);
+    run<0, 8, 1, 2, 1>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 1>("reg", b, G, per_wg, slice, iters);
+    run<0, 8, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
+  } else {
+    // cache policies at U = 16, 2 -> 2: loads (nt mask), stores (output, FIFO)
+    run<0, 16, 1, 2, 2, 0, kPlain, kPlain>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2, 1, kNonTemporal, kPlain>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2, 3, kNonTemporal, kPlain>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2, 3, kNonTemporal, kNonTemporal>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2, 1, kWriteThrough, kPlain>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2, 1, kNonTemporal, kWriteThrough>("reg", b, G, per_wg, slice, iters);
+    run<0, 12, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
+    run<0, 8, 1, 2, 2, 0, kPlain, kPlain>("reg", b, G, per_wg, slice, iters);
+    run<0, 8, 1, 2, 2, 3, kNonTemporal, kNonTemporal>("reg", b, G, per_wg, slice, iters);
+  }
   return 0;
 }
