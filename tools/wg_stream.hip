@@ -45,12 +45,17 @@ using namespace mccs;
 
 constexpr int kBlock = 544;
 
-// design: 0 reg, 1 regpp, 2 lds.  NTM: nt mask of the loads (bit 0 source 0,
+// design: 0 reg, 1 regpp, 2 lds, 3 reg with dynamic wave units (ring_stream.h).  NTM: nt mask of the loads (bit 0 source 0,
 // bit 1 source 1); P0 / P1: store policy of destination 0 / 1 (reduce_copy.h)
 template <int DES, int U, int S, int NS, int ND, int NTM = 1, int P0 = kNonTemporal, int P1 = kPlain>
 __global__ void __launch_bounds__(576) stream_kernel(const float* s0, const float* s1, float* d0, float* d1,
                                                      long per_wg, long slice) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t ctr[2];  // design 3: per-parity unit counters
+  uint32_t cbase[2] = {0, 0};
+  if (threadIdx.x == 0) ctr[0] = ctr[1] = 0;
+  __syncthreads();
+  int t = 0;
   const long base = (long)blockIdx.x * per_wg;
   const int nthr = blockDim.x;
   const int ndthr = (nthr / 64) * 64 == nthr ? nthr - 64 : (nthr / 64) * 64;  // whole waves, minus control
@@ -68,6 +73,9 @@ __global__ void __launch_bounds__(576) stream_kernel(const float* s0, const floa
         reduce_copy_rows<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr, false, none);
       } else if constexpr (DES == 1) {
         reduce_copy_rows_pp<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr);
+      } else if constexpr (DES == 3) {
+        cbase[t & 1] += reduce_copy_rows_dyn<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(
+            a, b, x, y, n, threadIdx.x, ndthr, &ctr[t & 1], cbase[t & 1]);
       } else {
         const uint32_t lds = (uint32_t)(uintptr_t)smem + (uint32_t)(wave * S * NS * U * 1024);
         lds_stream_rows<mccsFloat32, OpSum, U, S, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr, lds);
@@ -75,6 +83,7 @@ __global__ void __launch_bounds__(576) stream_kernel(const float* s0, const floa
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    ++t;
   }
 }
 
@@ -153,7 +162,8 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, b.s0, total, 1.0f);
   hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, b.s1, total, 5.0f);
   CK(hipDeviceSynchronize());
-  bool ok = check<0, 8, 1>(b, 1000003) && check<1, 4, 1>(b, 1000003) && check<1, 8, 1>(b, 1000003) &&
+  bool ok = check<0, 8, 1>(b, 1000003) && check<3, 8, 1>(b, 1000003) && check<3, 16, 1>(b, 3000017) &&
+            check<1, 4, 1>(b, 1000003) && check<1, 8, 1>(b, 1000003) &&
             check<2, 4, 2>(b, 1000003) && check<2, 2, 4>(b, 1000003) && check<2, 2, 3>(b, 1000003);
   std::printf("{\"check\": \"%s\"}\n", ok ? "ok" : "FAIL");
   std::fflush(stdout);
@@ -168,6 +178,28 @@ int main(int argc, char** argv) {
     run<0, 16, 1, 2, 1>("reg", b, G, per_wg, slice, iters);
     run<0, 8, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
     run<0, 16, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
+  } else if (set == 3) {
+    // static rows vs dynamic wave units, per slice shape
+    run<0, 8, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
+    run<3, 8, 1, 2, 2>("dyn", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
+    run<3, 16, 1, 2, 2>("dyn", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 1, 1>("reg", b, G, per_wg, slice, iters);
+    run<3, 16, 1, 1, 1>("dyn", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
+    run<3, 16, 1, 1, 2>("dyn", b, G, per_wg, slice, iters);
+  } else if (set == 2) {
+    // single-source slices (send 1 -> 1, recvCopySend 1 -> 2, recv 1 -> 1) at
+    // the register budget of a 2-source pass: twice the packs
+    run<0, 8, 1, 1, 1>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 1, 1>("reg", b, G, per_wg, slice, iters);
+    run<0, 32, 1, 1, 1>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
+    run<0, 32, 1, 1, 2>("reg", b, G, per_wg, slice, iters);
+    run<2, 8, 2, 1, 1>("lds", b, G, per_wg, slice, iters);
+    run<2, 8, 2, 1, 2>("lds", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 1>("reg", b, G, per_wg, slice, iters);
+    run<0, 16, 1, 2, 2>("reg", b, G, per_wg, slice, iters);
   } else {
     // cache policies at U = 16, 2 -> 2: loads (nt mask), stores (output, FIFO)
     run<0, 16, 1, 2, 2, 0, kPlain, kPlain>("reg", b, G, per_wg, slice, iters);
