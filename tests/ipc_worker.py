@@ -95,7 +95,12 @@ def main():
                 print(f"[rank {rank}] {mode} code={code}: {e}", flush=True)
                 ok = False
             if mode in direct_kw:  # the call really took that kernel
-                want = "oneshot" if mode == "ll" and count * vnode.ESIZE[code] > 1 << 20 else mode
+                # LL runs on uncached arenas only: where a rank's IPC export of
+                # its uncached arena was refused (the library then falls back to
+                # a hipMalloc arena + system fences on every rank, api.cpp
+                # mccsCommSetupRank) the bucket takes the one-shot instead
+                ll_ok = comm.fifo_memory != C.FIFO_DEVICE
+                want = "oneshot" if mode == "ll" and (count * vnode.ESIZE[code] > 1 << 20 or not ll_ok) else mode
                 ok = ok and comm.last_algo() == want
             results[f"{mode}/dtype{code}/n{count}"] = ok
         if mode in direct_kw:  # several launches back to back, fresh inputs each, then one sync
