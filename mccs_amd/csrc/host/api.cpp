@@ -346,6 +346,7 @@ extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks,
   h.fifo_slots = c->cfg.fifo_slots;
   h.slice_steps = c->slice_steps;
   h.block_threads = c->block_threads;
+  h.gate_env = gate_env();
   if (hipDeviceGetPCIBusId(h.pci, sizeof(h.pci) - 1, device) != hipSuccess) {
     (void)hipGetLastError();
     std::snprintf(h.pci, sizeof(h.pci), "ordinal:%d", device);
@@ -372,6 +373,9 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
         h.ll_bytes != c->cfg.ll_bytes || h.fifo_slots != c->cfg.fifo_slots || h.slice_steps != c->slice_steps ||
         h.block_threads != c->block_threads)
       return mccsInvalidArgument;
+    // the node gate's collectives need every rank (a rank that skipped it
+    // would leave the others in its vote until the watchdog)
+    if (h.gate_env != hs[c->rank].gate_env) return mccsInvalidArgument;
     all_uc = all_uc && h.fifo_memory != MCCS_FIFO_DEVICE;
     release = release || h.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
     if (h.lanes != hs[0].lanes || h.lanes_auto != hs[0].lanes_auto) return mccsInvalidArgument;

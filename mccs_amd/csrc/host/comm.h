@@ -104,6 +104,7 @@ struct ConnectHandle {
   // depth and the slice size.  Connect refuses any mismatch.
   int32_t direct_bytes, oneshot_bytes, ll_bytes;
   int32_t fifo_slots, slice_steps, block_threads;
+  int32_t gate_env;  // MCCS_GATE as this rank read it (-1 unset): every rank must run the node gate or none
   // PCI bus id of the rank's GPU: device ordinals are local to a process
   // (HIP_VISIBLE_DEVICES), so co-location and peer lookups use this
   char pci[32];
@@ -229,6 +230,7 @@ int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live l
 void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
 // gate.cpp
 bool gate_wanted(bool distinct_gpus);
+int gate_env();  // MCCS_GATE: -1 unset, else its value
 mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_ok);
 // plan.cpp
 void plan_discard(Comm* c);  // drops the pending plan

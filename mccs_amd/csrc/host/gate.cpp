@@ -219,10 +219,15 @@ mccsResult_t gate_vote(std::vector<Comm*>& cs, std::vector<Buf>& bufs, std::vect
 
 }  // namespace
 
-bool gate_wanted(bool distinct_gpus) {
+int gate_env() {
   const char* g = std::getenv("MCCS_GATE");
-  if (g && std::atoi(g) == 0) return false;
-  if (g && std::atoi(g) == 1) return true;
+  return g ? std::atoi(g) : -1;
+}
+
+bool gate_wanted(bool distinct_gpus) {
+  const int g = gate_env();
+  if (g == 0) return false;
+  if (g == 1) return true;
   return distinct_gpus;
 }
 
