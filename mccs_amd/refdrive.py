@@ -85,6 +85,7 @@ def libc() -> ctypes.CDLL:
         c.shm_open.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint]
         c.shm_unlink.argtypes = [ctypes.c_char_p]
         c.ftruncate.argtypes = [ctypes.c_int, ctypes.c_long]
+        c.posix_fallocate.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_long]
         c.mmap.argtypes = [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
         c.mmap.restype = vp
         c.munmap.argtypes = [vp, sz]
@@ -119,6 +120,12 @@ class HostSegment:
         try:
             if create and c.ftruncate(self._fd, self.nbytes) != 0:
                 raise OSError(ctypes.get_errno(), "ftruncate")
+            # reserve the pages now: a full /dev/shm then fails here (ENOSPC)
+            # instead of a SIGBUS at the first touch of an unbacked page
+            if create:
+                rc = c.posix_fallocate(self._fd, 0, self.nbytes)
+                if rc != 0:
+                    raise OSError(rc, f"posix_fallocate({self.nbytes} bytes of /dev/shm)")
             p = c.mmap(None, self.nbytes, 0x1 | 0x2, 0x01, self._fd, 0)  # PROT_READ|WRITE, MAP_SHARED
             if p in (None, ctypes.c_void_p(-1).value):
                 raise OSError(ctypes.get_errno(), "mmap")
