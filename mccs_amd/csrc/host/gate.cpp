@@ -20,14 +20,17 @@
 // verdicts travel through one ring AllReduce(MAX) in the cached mode with
 // system-scope fences, so all ranks step down together.  The same vote ANDs
 // the ranks' own view of peer atomics (each rank judged it from
-// device ordinals that are local to its process).  A gate launch that hits
-// the watchdog fails the connect with mccsTimeout: a hang leaves the FIFO
-// steps of the ranks out of step, which no local reset repairs.
+// device ordinals that are local to its process).  A direct test launch that
+// hits the (5 s) watchdog counts as a wrong sum for that variant; a ring
+// launch that does fails the connect with mccsTimeout (a hang leaves the
+// ranks' FIFO steps out of step, which no local reset repairs).
 //
 // MCCS_GATE=0 skips the gate; MCCS_GATE=1 runs it even when every rank is on
 // one GPU (tests).  Test seams, honoured only with MCCS_TEST_HOOKS=1:
 // MCCS_GATE_INJECT (a mask of MCCS_GATE_* bits treated as wrong sums on the
-// ranks named by MCCS_GATE_INJECT_RANK, default every rank) and
+// ranks named by MCCS_GATE_INJECT_RANK, default every rank), MCCS_GATE_SKIP
+// (direct paths those ranks do not launch, so their peers' launches hang
+// until the watchdog) and
 // MCCS_GATE_ASSUME_PASS=1 (the fake runtime runs no kernel: results are
 // taken as correct).  mccsCommGateInfo reports the outcome.
 #include <algorithm>
@@ -47,14 +50,20 @@ bool hooks_on() {
   return h && std::atoi(h) == 1;
 }
 
-unsigned injected(int rank) {
+unsigned hook_mask(const char* var, int rank) {
   if (!hooks_on()) return 0;
-  const char* m = std::getenv("MCCS_GATE_INJECT");
+  const char* m = std::getenv(var);
   if (!m) return 0;
   const char* r = std::getenv("MCCS_GATE_INJECT_RANK");
   if (r && std::atoi(r) != rank) return 0;
   return (unsigned)std::strtoul(m, nullptr, 0);
 }
+// paths reported wrong on this rank (MCCS_GATE_INJECT)
+unsigned injected(int rank) { return hook_mask("MCCS_GATE_INJECT", rank); }
+// direct paths this rank does not launch at all (MCCS_GATE_SKIP): its peers'
+// launches of them then hang until the watchdog, the failure mode of a
+// variant whose hand-off never arrives
+unsigned skipped(int rank) { return hook_mask("MCCS_GATE_SKIP", rank); }
 
 bool assume_pass() {
   const char* a = std::getenv("MCCS_GATE_ASSUME_PASS");
@@ -81,6 +90,7 @@ struct Buf {
 // Test sizes (fp32 elements per rank; ragged so tails are exercised) and the
 // algorithm the planner must report for each path.
 constexpr size_t kRingCount = 262144 + 3007;  // ~1 MiB: every channel, several slices
+constexpr uint64_t kGateTimeoutTicks = 500000000ull;  // 5 s (s_memrealtime, 100 MHz) per gate launch
 size_t path_count(const Comm* c, unsigned bit) {
   switch (bit) {
     case MCCS_GATE_LL: return std::min<size_t>((size_t)c->cfg.ll_bytes, 65536) / 4 - 1;
@@ -129,7 +139,7 @@ bool path_enabled(const Comm* c, unsigned bit) {
 // (fused per device), repetition `rep`.  ok[k]: rank slot k's output matched
 // and the planner took `want_algo`.
 mccsResult_t gate_allreduce(std::vector<Comm*>& cs, std::vector<Buf>& bufs, size_t count, int rep, int want_algo,
-                            std::vector<bool>* ok) {
+                            std::vector<bool>* ok, std::vector<bool>* hung_out) {
   const int n = cs[0]->nranks;
   std::vector<float> host(count), want(count);
   for (size_t i = 0; i < count; ++i) {
@@ -150,29 +160,69 @@ mccsResult_t gate_allreduce(std::vector<Comm*>& cs, std::vector<Buf>& bufs, size
   const mccsResult_t ge = mccsGroupEnd();
   MCCS_CHECK(er);
   MCCS_CHECK(ge);
-  for (Comm* c : cs) MCCS_CHECK(mccsCommSync((mccsComm_t)c));
+  // A direct launch that hits the watchdog is a wrong answer for that path,
+  // not a dead communicator: the direct kernel keeps no state the ring uses
+  // (its region is never touched again once the vote disables it), so the
+  // rank clears its abort line and votes.  A ring launch that hangs leaves
+  // the ranks' FIFO steps out of step: that one fails the connect.
+  std::vector<bool> hung(cs.size(), false);
+  for (size_t k = 0; k < cs.size(); ++k) {
+    Comm* c = cs[k];
+    const mccsResult_t sr = mccsCommSync((mccsComm_t)c);
+    if (sr == mccsSuccess) continue;
+    if (want_algo == MCCS_ALGO_RING || (sr != mccsTimeout && sr != mccsRemoteError)) return sr;
+    MCCS_LOG("node gate: a direct AllReduce (algo %d) hit the watchdog on rank %d; voting it off", want_algo, c->rank);
+    DeviceGuard g(c->device);
+    const uint32_t zero[2] = {0, 0};
+    MCCS_HIP(rt().Memcpy(c->d_abort, zero, sizeof(zero), hipMemcpyHostToDevice));
+    c->failed = false;
+    hung[k] = true;
+  }
   const bool pass = assume_pass();
   for (size_t k = 0; k < cs.size(); ++k) {
     DeviceGuard g(cs[k]->device);
     MCCS_HIP(rt().Memcpy(host.data(), bufs[k].recv, count * 4, hipMemcpyDeviceToHost));
     const bool same = pass || std::memcmp(host.data(), want.data(), count * 4) == 0;
-    (*ok)[k] = same && cs[k]->last_algo == want_algo;
+    (*ok)[k] = same && !hung[k] && cs[k]->last_algo == want_algo;
+    if (hung[k]) (*hung_out)[k] = true;
   }
   return mccsSuccess;
 }
 
 // Failure bits of `bit`'s path for every comm of `cs` (2 repetitions; ring 3).
-mccsResult_t gate_path(std::vector<Comm*>& cs, std::vector<Buf>& bufs, unsigned bit, std::vector<unsigned>* fail) {
+// `direct_dead`: a direct launch hung on one of these ranks earlier; the
+// direct variants share one control block (launch sequence, running counts)
+// that a hang leaves out of step, so none is launched again and all of them
+// are reported wrong (the vote turns them off on every rank).
+mccsResult_t gate_path(std::vector<Comm*>& cs, std::vector<Buf>& bufs, unsigned bit, std::vector<unsigned>* fail,
+                       bool* direct_dead) {
+  constexpr unsigned kDirect = MCCS_GATE_LL | MCCS_GATE_ONESHOT | MCCS_GATE_TWOSHOT;
+  const bool direct = bit & kDirect;
+  bool skip = direct && *direct_dead;
+  for (Comm* c : cs) skip = skip || (direct && (skipped(c->rank) & bit));
+  if (skip) {
+    for (unsigned& f : *fail) f |= kDirect;
+    *direct_dead = true;
+    return mccsSuccess;
+  }
   std::vector<Route> routes;
   routes.reserve(cs.size());
   for (Comm* c : cs) routes.emplace_back(c, bit);
   const size_t count = path_count(cs[0], bit);
-  const int reps = (bit & (MCCS_GATE_RING_UNCACHED | MCCS_GATE_RING_RELEASE | MCCS_GATE_RING_SYSTEM)) ? 3 : 2;
-  std::vector<bool> ok(cs.size(), true);
+  const int reps = direct ? 2 : 3;
+  std::vector<bool> ok(cs.size(), true), hung(cs.size(), false);
   for (int rep = 0; rep < reps; ++rep) {
-    MCCS_CHECK(gate_allreduce(cs, bufs, count, rep, path_algo(bit), &ok));
-    for (size_t k = 0; k < cs.size(); ++k)
+    MCCS_CHECK(gate_allreduce(cs, bufs, count, rep, path_algo(bit), &ok, &hung));
+    bool any_hung = false;
+    for (size_t k = 0; k < cs.size(); ++k) {
       if (!ok[k]) (*fail)[k] |= bit;
+      if (hung[k]) any_hung = true;
+    }
+    if (any_hung) {
+      for (unsigned& f : *fail) f |= kDirect;
+      *direct_dead = true;
+      break;
+    }
   }
   for (size_t k = 0; k < cs.size(); ++k) (*fail)[k] |= injected(cs[k]->rank) & bit;
   return mccsSuccess;
@@ -199,6 +249,9 @@ mccsResult_t gate_vote(std::vector<Comm*>& cs, std::vector<Buf>& bufs, std::vect
   Route route(c, 0);
   const mccsRingKernelCfg saved = c->kcfg;
   c->kcfg.fence_mode = MCCS_FENCE_SYSTEM;
+  // a peer may still sit in a direct test launch until its own (5 s)
+  // watchdog fires before this ring launch runs there: wait longer here
+  c->kcfg.timeout_ticks = 3ull * kGateTimeoutTicks;
   mccsResult_t r = mccsAllReduce(bufs[0].send, bufs[0].recv, kBits, mccsUint32, mccsDevMax, (mccsComm_t)c, nullptr);
   if (r == mccsSuccess) r = mccsCommSync((mccsComm_t)c);
   c->kcfg = saved;
@@ -247,9 +300,10 @@ mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_
       r = mccsUnhandledCudaError;
     // a gate launch that hangs ends after 5 s, not the configured 30 s
     saved_ticks[k] = cs[k]->kcfg.timeout_ticks;
-    if (saved_ticks[k] == 0 || saved_ticks[k] > 500000000ull) cs[k]->kcfg.timeout_ticks = 500000000ull;
+    if (saved_ticks[k] == 0 || saved_ticks[k] > kGateTimeoutTicks) cs[k]->kcfg.timeout_ticks = kGateTimeoutTicks;
   }
   unsigned failed = 0, disabled = 0;
+  bool direct_dead = false;
   std::vector<unsigned> fail(cs.size(), 0);
   // peer atomics: a rank that cannot do them turns the count-based variants off everywhere
   for (size_t k = 0; k < cs.size(); ++k)
@@ -257,7 +311,7 @@ mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_
   // 1. the ring, stepping down the hand-off ladder until every rank's sums are exact
   for (int attempt = 0; attempt < 3 && r == mccsSuccess; ++attempt) {
     const unsigned bit = ring_bit(cs[0]->kcfg.fence_mode);
-    r = gate_path(cs, bufs, bit, &fail);
+    r = gate_path(cs, bufs, bit, &fail, &direct_dead);
     unsigned agreed = 0;
     if (r == mccsSuccess) r = gate_vote(cs, bufs, &fail, &agreed);
     if (r != mccsSuccess) break;
@@ -289,7 +343,7 @@ mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_
     for (unsigned b : bits) {
       if (!path_enabled(cs[0], b) || r != mccsSuccess) continue;
       any = true;
-      r = gate_path(cs, bufs, b, &fail);
+      r = gate_path(cs, bufs, b, &fail, &direct_dead);
     }
     unsigned agreed = 0;
     if (r == mccsSuccess && any) r = gate_vote(cs, bufs, &fail, &agreed);

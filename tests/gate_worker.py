@@ -14,6 +14,11 @@ fresh communicator:
              release mode together;
   oneshot    rank 0 alone reports a wrong one-shot sum: every rank disables
              the one-shot, its buckets take the ring on every rank;
+  hang       rank 1 does not launch the LL test (MCCS_GATE_SKIP), so rank 0's
+             LL kernel waits for lines that never come until the 5 s watchdog:
+             a hang in a direct variant is a vote against every direct
+             variant (they share one control block), not a dead communicator;
+             both ranks keep the ring, exact;
   mismatch   ranks resolve different one-shot thresholds that round to the
              same arena: Connect refuses on every rank.
 After each connect, exact-sum AllReduces at LL / one-shot / ring sizes check
@@ -26,7 +31,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-G_RING_UC, G_ONE = 0x1, 0x10
+G_RING_UC, G_LL, G_ONE, G_TWO = 0x1, 0x8, 0x10, 0x20
 
 
 def main():
@@ -50,12 +55,13 @@ def main():
     os.environ["MCCS_TEST_HOOKS"] = "1"
     cases = {"clean": {}, "ring": {"MCCS_GATE_INJECT": hex(G_RING_UC), "MCCS_GATE_INJECT_RANK": "1"},
              "oneshot": {"MCCS_GATE_INJECT": hex(G_ONE), "MCCS_GATE_INJECT_RANK": "0"},
+             "hang": {"MCCS_GATE_SKIP": hex(G_LL), "MCCS_GATE_INJECT_RANK": "1"},
              "mismatch": {"MCCS_ONESHOT_BYTES": "1000000" if rank == 0 else "1048576"}}
     results = {}
     dv = torch.device("cuda", dev)
     for name, env in cases.items():
-        for k in ("MCCS_GATE_INJECT", "MCCS_GATE_INJECT_RANK", "MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES",
-                  "MCCS_LL_BYTES"):
+        for k in ("MCCS_GATE_INJECT", "MCCS_GATE_SKIP", "MCCS_GATE_INJECT_RANK", "MCCS_ONESHOT_BYTES",
+                  "MCCS_DIRECT_BYTES", "MCCS_LL_BYTES"):
             os.environ.pop(k, None)
         os.environ.update(env)
         dist.barrier()
@@ -71,13 +77,14 @@ def main():
         gi = comm.gate_info()
         want_mode = 2 if name == "ring" else 0  # MCCS_FIFO_UNCACHED_RELEASE / MCCS_FIFO_UNCACHED
         ok = gi["ran"] and gi["fifo_mode"] == want_mode and comm.fifo_memory == want_mode
-        ok = ok and gi["disabled"] == (G_ONE if name == "oneshot" else 0)
+        want_off = {"oneshot": G_ONE, "hang": G_LL | G_ONE | G_TWO}.get(name, 0)
+        ok = ok and gi["disabled"] == want_off
         ok = ok and (gi["failed"] & G_RING_UC) == (G_RING_UC if name == "ring" else 0)
         results[f"{name}/gate"] = {"ok": bool(ok), "info": gi}
         # LL-sized, one-shot-sized and ring-sized buckets (defaults at n = 2:
         # LL <= 128 KiB, one-shot <= 2 MiB, two-shot off)
-        for nbytes, algo in ((32 << 10, "ll"), (512 << 10, "ring" if name == "oneshot" else "oneshot"),
-                             (8 << 20, "ring")):
+        for nbytes, algo in ((32 << 10, "ring" if name == "hang" else "ll"),
+                             (512 << 10, "ring" if name in ("oneshot", "hang") else "oneshot"), (8 << 20, "ring")):
             count = nbytes // 4
             send = refdrive.exact_inputs(torch, count, rank, torch.float32, dv)
             want = refdrive.expected_exact(torch, count, world, torch.float32, dv)

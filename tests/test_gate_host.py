@@ -44,7 +44,8 @@ def gate(monkeypatch):
     lib = _lib.load()
     monkeypatch.setenv("MCCS_TEST_HOOKS", "1")
     monkeypatch.setenv("MCCS_GATE_ASSUME_PASS", "1")
-    for v in ("MCCS_GATE", "MCCS_GATE_INJECT", "MCCS_GATE_INJECT_RANK", "MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES",
+    for v in ("MCCS_GATE", "MCCS_GATE_INJECT", "MCCS_GATE_SKIP", "MCCS_GATE_INJECT_RANK", "MCCS_ONESHOT_BYTES",
+              "MCCS_DIRECT_BYTES",
               "MCCS_LL_BYTES", "MCCS_FIFO_MEMORY"):
         monkeypatch.delenv(v, raising=False)
     made = []
@@ -207,3 +208,20 @@ def test_nonzero_reserved_word_is_refused(monkeypatch):
         assert lib.mccsCommInitAll(comms, 2, devs, ctypes.byref(cfg)) == 4
     finally:
         lib.mccs_test_fake_runtime(0)
+
+
+def test_a_hung_direct_path_turns_every_direct_variant_off(gate, monkeypatch):
+    """A direct launch that hangs (here: never launched, MCCS_GATE_SKIP) is a
+    vote against every direct variant -- they share one control block -- and
+    the gate launches no further direct test; the ring stays."""
+    monkeypatch.setenv("MCCS_GATE_SKIP", hex(G_LL))
+    comms = gate(4)
+    ls = _gate_launches(_log())
+    assert {kv["kind"] for kv in ls} == {"ring"}  # no direct test launched after the LL one was skipped
+    for c in comms:
+        gi = c.gate_info()
+        assert gi["disabled"] == G_LL | G_ONE | G_TWO and gi["fifo_mode"] == FIFO_UNCACHED
+    with C.group():
+        for r, c in enumerate(comms):
+            C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 8192, F32, SUM, stream=0)
+    assert {kv["kind"] for kv in _gate_launches(_log())} == {"ring"}

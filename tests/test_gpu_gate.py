@@ -4,7 +4,9 @@ Two ranks as two processes on the one-GPU box with the gate forced on
 (MCCS_GATE=1): a clean pass keeps every default path; a wrong ring sum
 injected on one rank steps both down to the release hand-off through the
 ring vote; a wrong one-shot sum injected on the other rank disables the
-one-shot on both; thresholds that differ but round to the same arena make
+one-shot on both; a direct launch left hanging (the peer never launches it)
+ends at the 5 s watchdog as a vote against every direct variant while the
+ring stays usable; thresholds that differ but round to the same arena make
 Connect refuse on both.  Every AllReduce after a gate is
 checked exact and for the kernel it took.
 """
@@ -36,4 +38,4 @@ def test_gate_verdicts_agree_across_processes():
     assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(lines[-1])
     assert res["all_ok"], res
-    assert set(res["cases"]) >= {"clean/gate", "ring/gate", "oneshot/gate", "mismatch/connect"}
+    assert set(res["cases"]) >= {"clean/gate", "ring/gate", "oneshot/gate", "hang/gate", "mismatch/connect"}
