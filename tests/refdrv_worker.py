@@ -81,6 +81,29 @@ def main():
                     ok = ok and int(exp[0]) == 2042 * n + n * (n - 1) // 2
                 results[f"{vname}/dtype{code}/n{count}/rep{rep}"] = {"ok": ok, "steps": rr.steps()}
                 del send, recv
+        if vname == "ref_sender":
+            # every (dtype, op) kernel the reference names, at a ragged count
+            # that takes several passes and a tail per slice (the reference-
+            # named kernels stream 16 packs per source, bf16 12, bytes 4:
+            # a code path of their own, ring_kernel.h kRefUnroll)
+            for code in range(10):
+                for op in range(4):
+                    count = 150001 + 17 * code + op
+                    rng = np.random.default_rng(1000 * code + 10 * op + rank)
+                    x = vnode.gen(code, count, rng)
+                    xs = allgather(x)
+                    send, recv = vnode.to_dev(x), vnode.to_dev(np.zeros_like(x))
+                    torch.cuda.synchronize()
+                    dist.barrier()
+                    rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, op, stream.cuda_stream)
+                    stream.synchronize()
+                    k, nthr, ring_used = rr.last_plan
+                    exp = orc.ring_allreduce(code, op, xs, nchannels=k, nthreads=nthr, buff_size=rr.buff,
+                                             ring_orders=ring_used)
+                    got = vnode.from_dev(recv, code)
+                    ok = bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8))) and not rr.aborted()
+                    results[f"{vname}/all_kernels/dtype{code}/op{op}"] = {"ok": ok, "steps": rr.steps()}
+                    del send, recv
         # 1100 back-to-back 4 KiB launches (one channel, one work entry each):
         # the 1024-entry work ring wraps and the host waits on workFifoDone
         count = 1024
