@@ -237,8 +237,11 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
             continue
         seen.add(key)
         el = max_over_ranks(dist, time_steps(torch, dist, comm, step_for(comm), warmup, reps))
+        # fifo_memory_run: the hand-off the candidate really ran after the
+        # connect-time node gate (0 uncached, 1 cached + system fences,
+        # 2 uncached + release), which may be safer than its mode's name
         table.append({"mode": mode, "channels": comm.nchannels, "lanes": comm.lanes,
-                      "ms_per_step": round(el / reps * 1e3, 4)})
+                      "fifo_memory_run": comm.fifo_memory, "ms_per_step": round(el / reps * 1e3, 4)})
         if best is None or el < best[0]:
             if best is not None:
                 best[1].destroy()
