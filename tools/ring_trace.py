@@ -34,13 +34,25 @@ def main():
     ap.add_argument("--mib", type=int, default=128)
     ap.add_argument("--kib", type=int, default=0, help="bucket size in KiB (overrides --mib)")
     ap.add_argument("--show", type=int, default=12, help="slices printed per rank")
+    ap.add_argument("--per-wave", action="store_true", help="per data wave split of each slice (rank 0)")
+    ap.add_argument("--channels", type=int, default=0, help="channel count (0: default)")
+    ap.add_argument("--ref-shape", action="store_true", help="the reference launch shape (see below)")
     args = ap.parse_args()
     lib = _lib.load()
     fn = lib.mccs_ring_trace_ar_sum
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     fn.restype = ctypes.c_int
     n = args.n
-    comms = C.init_all([0] * n, C.CommConfig(lanes=args.lanes))
+    kw = {"channel_count": args.channels} if args.channels else {}
+    if args.ref_shape:
+        # the reference launch shape through the library: 2 channels x one
+        # 544-thread workgroup, 8 slots of a 4 MiB buffer, 2-step slices,
+        # cached FIFOs with system-scope fences (kRefCfg)
+        os.environ["MCCS_SLICE_STEPS"] = "2"
+        kw = dict(channel_count=2, block_threads=544, fifo_slots=8, buffer_size=4 << 20,
+                  fifo_memory=C.FIFO_DEVICE)
+        args.lanes = 1
+    comms = C.init_all([0] * n, C.CommConfig(lanes=args.lanes, **kw))
     cnt = ((args.kib << 10) if args.kib else (args.mib << 20)) // 4
     xs = [torch.randn(cnt, device="cuda") for _ in range(n)]
     ys = [torch.empty_like(x) for x in xs]
@@ -102,6 +114,41 @@ def main():
         per.sort()
         print(json.dumps({"detect_ticks_median": lat[len(lat) // 2], "detect_ticks_p90": lat[9 * len(lat) // 10],
                           "start_to_post_ticks_median": per[len(per) // 2]}))
+    if args.per_wave:
+        # where a slice's time goes, per data wave (rank 0): start -> issued
+        # (streaming), issued -> drained (the drain), drained -> added (waiting
+        # for the other waves to count out of the previous slice), and the
+        # slice's span from its first start to its post
+        g = ev[0]
+        rows = []
+        for t in range(3, nsl):
+            st = dict((w, x) for x, w in g.get((t, "start"), []))
+            iss = dict((w, x) for x, w in g.get((t, "issued"), []))
+            dr = dict((w, x) for x, w in g.get((t, "drained"), []))
+            ad = dict((w, x) for x, w in g.get((t, "added"), []))
+            po = min((x for x, _ in g.get((t, "post"), [])), default=None)
+            waves = sorted(set(st) & set(iss) & set(dr) & set(ad))
+            if not waves or po is None:
+                continue
+            s0 = min(st[w] for w in waves)
+            rows.append({"t": t, "span": po - s0,
+                         "start_skew": max(st[w] for w in waves) - s0,
+                         "stream": [iss[w] - st[w] for w in waves],
+                         "drain": [dr[w] - iss[w] for w in waves],
+                         "countout_wait": [ad[w] - dr[w] for w in waves]})
+        for r in rows[: args.show]:
+            print(json.dumps(r))
+        if rows:
+            import statistics as stt
+            print(json.dumps({
+                "per_wave_summary_ticks": {
+                    "span_median": stt.median(r["span"] for r in rows),
+                    "start_skew_median": stt.median(r["start_skew"] for r in rows),
+                    "stream_median": stt.median(x for r in rows for x in r["stream"]),
+                    "stream_max_median": stt.median(max(r["stream"]) for r in rows),
+                    "drain_median": stt.median(x for r in rows for x in r["drain"]),
+                    "countout_wait_median": stt.median(x for r in rows for x in r["countout_wait"]),
+                    "slices": len(rows)}}))
     for c in comms:
         c.destroy()
 
