@@ -121,7 +121,11 @@ __device__ __forceinline__ void reduce_copy_rows_pp(const void* s0, const void* 
 // of the workgroup decides alike).  Same operands and results as
 // reduce_copy_rows; no input prefetch (it serves slices shorter than one
 // pass of the static layout).
-template <int DT, int OP, int U, int NS, int ND, int NTMASK, int DP0 = kPlain, int DP1 = kPlain>
+#ifndef MCCS_RING_GRAB_AHEAD
+#define MCCS_RING_GRAB_AHEAD 0
+#endif
+template <int DT, int OP, int U, int NS, int ND, int NTMASK, int DP0 = kPlain, int DP1 = kPlain,
+          bool GRAB_AHEAD = MCCS_RING_GRAB_AHEAD>
 __device__ __forceinline__ uint32_t reduce_copy_rows_dyn(const void* s0, const void* s1, void* d0, void* d1,
                                                          int64_t nelem, int tid, int nthr, uint32_t* ctr,
                                                          uint32_t base) {
@@ -152,10 +156,14 @@ __device__ __forceinline__ uint32_t reduce_copy_rows_dyn(const void* s0, const v
   u32x4* y = (u32x4*)d1;
   const uint32_t unit = 64u * U;
   const uint32_t nunits = npack / unit;  // whole units; the rest below, by every wave
+  // GRAB_AHEAD: the next unit is taken while this one's loads are in
+  // flight, so the LDS atomic's round trip leaves the issue path (each wave
+  // still makes exactly one failing grab)
+  uint32_t g = 0;
+  if (GRAB_AHEAD && lane == 0) g = atomicAdd(ctr, 1u);
 #pragma unroll 1
   for (;;) {
-    uint32_t g = 0;
-    if (lane == 0) g = atomicAdd(ctr, 1u);
+    if (!GRAB_AHEAD && lane == 0) g = atomicAdd(ctr, 1u);
     const uint32_t k = __builtin_amdgcn_readfirstlane(g) - base;
     if (k >= nunits) break;
     // the unit's bases are uniform: saddr + lane offset addressing
@@ -171,6 +179,7 @@ __device__ __forceinline__ uint32_t reduce_copy_rows_dyn(const void* s0, const v
 #pragma unroll
       for (int u = 0; u < U; ++u) w[u] = ld16<LP1>(bk + lane + 64u * u);
     }
+    if (GRAB_AHEAD && lane == 0) g = atomicAdd(ctr, 1u);
     // every load of the unit is issued before the first use (the scheduler
     // would otherwise interleave waits to save registers: fewer bytes in flight)
     __builtin_amdgcn_sched_barrier(0);
