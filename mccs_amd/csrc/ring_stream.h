@@ -15,6 +15,7 @@
 // destination; 16-byte aligned operands (else the typed fallback); typed
 // scalar tail past the last whole pack.
 #pragma once
+#include <type_traits>
 #include <utility>
 
 #include "dtypes.h"
@@ -24,13 +25,24 @@
 namespace mccs {
 
 // A wave-uniform pointer the compiler cannot prove uniform, moved to SGPRs
-// (loads and stores then address saddr + a 32-bit lane offset).
+// (loads and stores then address saddr + a 32-bit lane offset).  The value
+// is rebuilt as a GLOBAL-address-space pointer and only then converted to a
+// generic one, so the compiler still sees global memory behind it: rebuilt
+// from an integer as a generic pointer it became flat_load / flat_store,
+// which count in lgkmcnt as well as vmcnt, so every LDS wait (a dynamic
+// unit's grab, the count-out) also waited for all of the wave's memory
+// operations in flight (gfx950 assembly of the ring kernels; one workgroup
+// streamed 58-63 GB/s that way against 75-89 with global operations).
+// Every operand behind it is global memory: device HBM, a peer's HBM or
+// host memory mapped for the device; never LDS or scratch.
 template <typename P>
 __device__ __forceinline__ P uniform_ptr(P p) {
+  using E = std::remove_pointer_t<P>;
   const uint64_t v = (uint64_t)(uintptr_t)p;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return (P)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  auto* g = (__attribute__((address_space(1))) E*)(((uint64_t)hi << 32) | lo);
+  return (P)g;
 }
 
 // Register double buffer.  Full passes alternate between two register sets
