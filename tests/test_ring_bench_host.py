@@ -61,7 +61,7 @@ def test_ring_line_schema(share):
     # ratio (virtual node) under its own name
     assert rf["traffic"] is None and rf["traffic_note"].startswith("not measured on the node")
     tv = rf["traffic_virtual_node_n2"]
-    assert tv["traffic_over_algorithmic"] == 1.0043 and "virtual node" in tv["where"]
+    assert tv["traffic_over_algorithmic"] == 1.0045 and "virtual node" in tv["where"]
     assert tv["source"].startswith("profiles/r04_ring_vnode_summary.json")
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and 0 < rf["frac"] <= 1
     if share:
