@@ -33,7 +33,10 @@ def test_multi_process_ring_matches_oracle(world, modes):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", IPC_MODES=modes)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=os.path.dirname(HERE))
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
+    # the library's own log lines first (a rank's setup error is otherwise cut
+    # off by the launcher's long tail)
+    lib_lines = "\n".join(l for l in (r.stdout + r.stderr).splitlines() if "mccs" in l.lower() or "hip" in l)[-3000:]
+    assert r.returncode == 0 and lines, lib_lines + "\n----\n" + r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(lines[-1])
     assert res["all_ok"], res
     assert res["world"] == world
