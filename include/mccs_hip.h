@@ -235,6 +235,18 @@ mccsResult_t mccsCommGateInfo(mccsComm_t comm, int *info4);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
 const char *mccsGetErrorString(mccsResult_t r);
+/* Diagnosis of the calling thread's latest failed library call: the step it
+ * failed in, the failing runtime call and its hipError_t name and text, e.g.
+ * "mccsCommSetupRank(rank 2/4, device 0) > comm_alloc_local > work FIFO:
+ * HostMallocMapped -> hipErrorOutOfMemory (out of memory) at comm.cpp:318".
+ * "" when the latest communicator / collective call succeeded (each one clears
+ * it on entry).  The pointer stays valid until this thread's next library
+ * call.  The reference returns one code per failure and logs the CUDA error
+ * (cuda_warning!, src/mccs/src/utils/mod.rs:7-26); this adds where it failed. */
+const char *mccsGetLastErrorString(void);
+/* The hipError_t of that failure (0 when the failure was not a HIP call, e.g.
+ * a refused argument or mismatched peers). */
+int mccsGetLastHipError(void);
 /* Ring timing counters of `device` (armed by MCCS_RING_PROFILE=1 at
  * communicator init): out4[0] slices, [1] ticks waiting for peer flags,
  * [2] ticks streaming + draining (s_memrealtime, 100 MHz), [3] reserved.

@@ -54,9 +54,13 @@ RESULT_NAMES = {
 
 
 class MccsError(RuntimeError):
-    def __init__(self, code: int, what: str):
+    """A failed C-ABI call: the result code, plus the library's own diagnosis
+    of where it failed (mccsGetLastErrorString: step, runtime call, hipError_t)."""
+
+    def __init__(self, code: int, what: str, detail: str = ""):
         self.code = code
-        super().__init__(f"{what}: {RESULT_NAMES.get(code, code)} ({code})")
+        self.detail = detail
+        super().__init__(f"{what}: {RESULT_NAMES.get(code, code)} ({code})" + (f" [{detail}]" if detail else ""))
 
 
 _c_void_p = ctypes.c_void_p
@@ -125,6 +129,8 @@ SIGNATURES: dict[str, tuple] = {
     "mccsEventRecordShared": (_c_int, [_c_void_p, _c_void_p]),
     "mccsStreamWaitShared": (_c_int, [_c_void_p, _c_void_p]),
     "mccsGetErrorString": (ctypes.c_char_p, [_c_int]),
+    "mccsGetLastErrorString": (ctypes.c_char_p, []),
+    "mccsGetLastHipError": (_c_int, []),
     "mccs_default_rings": (_c_int, [_c_int, _c_int, _P(_c_int), _c_int]),
     "mccs_task_schema": (None, [_c_size_t, _c_int, _P(_c_int), _P(_c_int)]),
     "mccs_direct_defaults": (None, [_c_int, _P(_c_int), _P(_c_int)]),
@@ -158,9 +164,16 @@ def load(path: str | None = None) -> ctypes.CDLL:
     return lib
 
 
+def last_error() -> str:
+    """The calling thread's diagnosis of its latest failed library call ("" if none)."""
+    return _lib.mccsGetLastErrorString().decode(errors="replace") if _lib is not None else ""
+
+
 def check(code: int, what: str) -> None:
+    """Raises MccsError for a nonzero result; call it right after the failed
+    call, on the same thread (the diagnosis is per thread)."""
     if code != 0:
-        raise MccsError(code, what)
+        raise MccsError(code, what, last_error())
 
 
 def ptr_array(ptrs) -> ctypes.Array:

@@ -21,6 +21,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import enum
+import time
 from dataclasses import dataclass
 
 from . import _lib
@@ -215,22 +216,37 @@ def init_communicator_rank(rank: int, nranks: int, device: int, exchange, config
     hsize = lib.mccsConnectHandleSize()
     mine = (ctypes.c_char * hsize)()
     h = ctypes.c_void_p()
+    t0 = time.perf_counter()
     rc = lib.mccsCommSetupRank(ctypes.byref(h), rank, nranks, device, ctypes.byref(cfg), mine)
+    detail = _lib.last_error() if rc != 0 else ""
+    t1 = time.perf_counter()
     del keep
-    # every rank joins the exchange even after a local failure (an empty
-    # handle), so a peer's error never leaves the others blocked in it
-    allh = exchange(bytes(mine) if rc == 0 else b"")
-    _lib.check(rc, "mccsCommSetupRank")
+    # every rank joins the exchange even after a local failure (its diagnosis
+    # in place of a handle), so a peer's error never leaves the others blocked
+    # in it, and every rank can say which rank failed and why
+    allh = exchange(bytes(mine) if rc == 0 else b"ERR:" + detail.encode())
+    if rc != 0:
+        raise _lib.MccsError(rc, "mccsCommSetupRank", detail)
     comm = Communicator(h.value)
     if len(allh) != nranks or any(len(x) != hsize for x in allh):
         comm.destroy()
-        raise RuntimeError("connect-handle exchange: a peer failed mccsCommSetupRank or sent malformed data")
+        failed = [(r, x[4:].decode(errors="replace")) for r, x in enumerate(allh) if x[:4] == b"ERR:"]
+        if failed:
+            raise RuntimeError("connect-handle exchange: " +
+                               "; ".join(f"rank {r} failed mccsCommSetupRank: {d}" for r, d in failed))
+        raise RuntimeError("connect-handle exchange: a peer sent malformed data")
     buf = ctypes.create_string_buffer(b"".join(allh), hsize * nranks)
+    t2 = time.perf_counter()
     rc = lib.mccsCommConnect(h, buf)
     if rc != 0:
+        detail = _lib.last_error()
         comm.destroy()
-        _lib.check(rc, "mccsCommConnect")
+        raise _lib.MccsError(rc, "mccsCommConnect", detail)
     comm._load_info()
+    # this rank's wall time per phase (the N > 1 bench line reports it per rank);
+    # connect includes the node gate when it runs
+    comm.connect_timing = {"setup_s": round(t1 - t0, 4), "exchange_s": round(t2 - t1, 4),
+                           "connect_s": round(time.perf_counter() - t2, 4)}
     return comm
 
 

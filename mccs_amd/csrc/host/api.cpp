@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "comm.h"
@@ -78,39 +79,50 @@ static void fill_defaults(mccsCommConfig* c, int nranks) {
 }
 
 static mccsResult_t validate_cfg(const mccsCommConfig& c, int nranks) {
+  StepScope st("config");
   // a chunk (buffer_size/2 bytes) must be a multiple of the largest thread
   // granule (512 x 8 B, all_reduce.h:34-35) so a rounded chunk fits 4 steps
-  if (c.buffer_size < 8192 || c.buffer_size % 8192 != 0) return mccsInvalidArgument;
+  if (c.buffer_size < 8192 || c.buffer_size % 8192 != 0)
+    MCCS_FAIL(mccsInvalidArgument, "buffer_size %d is not a multiple of 8192", c.buffer_size);
   // multiples of 32 keep the reference's nWarps*32 blocks (e.g. 544) valid;
   // at least one data wave next to the control wave (ring_kernel.h), like
   // the reference's smallest block (96 threads, plan.rs:602-635)
-  if (c.block_threads < 96 || c.block_threads > MCCS_RING_MAX_THREADS || c.block_threads % 32) return mccsInvalidArgument;
-  if (c.lanes < 0 || c.lanes > MCCS_MAX_LANES) return mccsInvalidArgument;
-  if (c.channel_count < 0 || c.channel_count > MCCS_MAX_NCHANNELS) return mccsInvalidArgument;
-  if (c.work_fifo_depth & (c.work_fifo_depth - 1)) return mccsInvalidArgument;
-  if (c.locality != MCCS_LOCALITY_SENDER && c.locality != MCCS_LOCALITY_RECEIVER) return mccsInvalidArgument;
+  if (c.block_threads < 96 || c.block_threads > MCCS_RING_MAX_THREADS || c.block_threads % 32)
+    MCCS_FAIL(mccsInvalidArgument, "block_threads %d outside 96..%d or not a multiple of 32", c.block_threads,
+              MCCS_RING_MAX_THREADS);
+  if (c.lanes < 0 || c.lanes > MCCS_MAX_LANES) MCCS_FAIL(mccsInvalidArgument, "lanes %d outside 0..%d", c.lanes, MCCS_MAX_LANES);
+  if (c.channel_count < 0 || c.channel_count > MCCS_MAX_NCHANNELS)
+    MCCS_FAIL(mccsInvalidArgument, "channel_count %d outside 0..%d", c.channel_count, MCCS_MAX_NCHANNELS);
+  if (c.work_fifo_depth & (c.work_fifo_depth - 1))
+    MCCS_FAIL(mccsInvalidArgument, "work_fifo_depth %d is not a power of two", c.work_fifo_depth);
+  if (c.locality != MCCS_LOCALITY_SENDER && c.locality != MCCS_LOCALITY_RECEIVER)
+    MCCS_FAIL(mccsInvalidArgument, "locality %d unknown", c.locality);
   if (c.fifo_memory != MCCS_FIFO_UNCACHED && c.fifo_memory != MCCS_FIFO_DEVICE &&
       c.fifo_memory != MCCS_FIFO_UNCACHED_RELEASE)
-    return mccsInvalidArgument;
-  if (nranks < 1 || nranks > 64) return mccsInvalidArgument;
-  if (c.fifo_slots != 8 && c.fifo_slots != 16 && c.fifo_slots != 32) return mccsInvalidArgument;
-  if (c.direct_bytes > (1 << 30)) return mccsInvalidArgument;    // 9 slots of it live in every rank's arena
-  if (c.oneshot_bytes > (64 << 20)) return mccsInvalidArgument;  // 16 slots of it
-  if (c.ll_bytes > (1 << 20)) return mccsInvalidArgument;        // 16 slots of twice it
+    MCCS_FAIL(mccsInvalidArgument, "fifo_memory %d unknown", c.fifo_memory);
+  if (nranks < 1 || nranks > 64) MCCS_FAIL(mccsInvalidArgument, "nranks %d outside 1..64", nranks);
+  if (c.fifo_slots != 8 && c.fifo_slots != 16 && c.fifo_slots != 32)
+    MCCS_FAIL(mccsInvalidArgument, "fifo_slots %d is not 8, 16 or 32", c.fifo_slots);
+  // 9 slots of direct_bytes, 16 of oneshot_bytes and 16 of twice ll_bytes live in every rank's arena
+  if (c.direct_bytes > (1 << 30)) MCCS_FAIL(mccsInvalidArgument, "direct_bytes %d above 1 GiB", c.direct_bytes);
+  if (c.oneshot_bytes > (64 << 20)) MCCS_FAIL(mccsInvalidArgument, "oneshot_bytes %d above 64 MiB", c.oneshot_bytes);
+  if (c.ll_bytes > (1 << 20)) MCCS_FAIL(mccsInvalidArgument, "ll_bytes %d above 1 MiB", c.ll_bytes);
   return mccsSuccess;
 }
 
 static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommConfig* user_cfg, Comm** out) {
+  StepScope st("make_comm");
   mccsCommConfig cfg;
   mccsCommConfigDefault(&cfg);
   if (user_cfg) cfg = *user_cfg;
   for (int w : cfg.reserved)
-    if (w != 0) return mccsInvalidArgument;  // a field this library does not know
+    if (w != 0) MCCS_FAIL(mccsInvalidArgument, "a reserved config word is not zero");  // a field this library does not know
   fill_defaults(&cfg, nranks);
   MCCS_CHECK(validate_cfg(cfg, nranks));
-  if (rank < 0 || rank >= nranks) return mccsInvalidArgument;
+  if (rank < 0 || rank >= nranks) MCCS_FAIL(mccsInvalidArgument, "rank %d outside 0..%d", rank, nranks - 1);
   int ndev = 0;
-  if (rt().GetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return mccsInvalidArgument;
+  MCCS_HIP(rt().GetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) MCCS_FAIL(mccsInvalidArgument, "device %d not visible (%d devices)", device, ndev);
   Comm* c = new Comm();
   c->rank = rank;
   c->nranks = nranks;
@@ -125,7 +137,8 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
       for (int i = 0; i < nranks; ++i)
         if (s[i] != i) {
           delete c;
-          return mccsInvalidArgument;  // not a permutation (engine.rs:274-279 asserts)
+          // not a permutation (engine.rs:274-279 asserts)
+          MCCS_FAIL(mccsInvalidArgument, "rings[%d] is not a permutation of 0..%d", ch, nranks - 1);
         }
       c->rings.push_back(r);
     }
@@ -148,7 +161,7 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   while (c->lanes > 1 && (size_t)cfg.buffer_size / MCCS_BUFFER_SLOTS * 2 / c->lanes < 256) {
     if (cfg.lanes > 0) {
       delete c;
-      return mccsInvalidArgument;
+      MCCS_FAIL(mccsInvalidArgument, "lanes %d leave under 256 bytes of a slot pair per lane", cfg.lanes);
     }
     c->lanes /= 2;
   }
@@ -158,19 +171,18 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
 
 static mccsResult_t enable_peer(int a, int b) {
   if (a == b) return mccsSuccess;
+  StepScope st("peer access " + std::to_string(a) + " -> " + std::to_string(b));
   int can = 0;
-  if (rt().CanAccessPeer(&can, a, b) != hipSuccess || !can) return mccsSystemError;
+  MCCS_HIP(rt().CanAccessPeer(&can, a, b));
+  if (!can) MCCS_FAIL(mccsSystemError, "device %d cannot access device %d", a, b);
   DeviceGuard g(a);
-  hipError_t e = rt().EnablePeerAccess(b);
-  if (e != hipSuccess) {
-    MCCS_LOG("hipDeviceEnablePeerAccess(%d -> %d): %s", a, b, hipGetErrorString(e));
-    return mccsUnhandledCudaError;
-  }
+  MCCS_HIP(rt().EnablePeerAccess(b));
   return mccsSuccess;
 }
 
 static mccsResult_t launch_single(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count,
                                   hipStream_t stream) {
+  err_clear();
   auto reject = [](mccsResult_t e) {
     if (g_group.depth > 0 && g_group.error == mccsSuccess) g_group.error = e;
     return e;
@@ -237,10 +249,15 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
 }
 
 extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {
-  if (!comms || !devices || nranks < 1) return mccsInvalidArgument;
+  err_clear();
+  StepScope st0("mccsCommInitAll(" + std::to_string(nranks) + " ranks)");
+  if (!comms || !devices || nranks < 1) MCCS_FAIL(mccsInvalidArgument, "null comms/devices or nranks < 1");
   std::vector<Comm*> cs(nranks, nullptr);
   mccsResult_t r = mccsSuccess;
-  for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = make_comm(i, nranks, devices[i], cfg, &cs[i]);
+  for (int i = 0; i < nranks && r == mccsSuccess; ++i) {
+    StepScope st("rank " + std::to_string(i));
+    r = make_comm(i, nranks, devices[i], cfg, &cs[i]);
+  }
   // ranks sharing a GPU run as one fused launch that must be co-resident:
   // shrink automatic lanes to fit (explicit lanes are checked at launch)
   for (int i = 0; i < nranks && r == mccsSuccess; ++i) {
@@ -251,10 +268,18 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
     if (share < 2 || c->cfg.lanes > 0) continue;
     const int cap = coresident_ring_blocks(c->block_threads, c->device);
     const int fit = cap / (share * c->nch);
-    if (fit < 1) r = mccsInvalidUsage;
-    else c->lanes = std::min(c->lanes, fit);
+    if (fit < 1) {
+      err_note(__FILE__, __LINE__, "%d ranks x %d channels do not fit %d co-resident workgroups on device %d", share,
+               c->nch, cap, c->device);
+      r = mccsInvalidUsage;
+    } else {
+      c->lanes = std::min(c->lanes, fit);
+    }
   }
-  for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_alloc_local(cs[i]);
+  for (int i = 0; i < nranks && r == mccsSuccess; ++i) {
+    StepScope st("rank " + std::to_string(i));
+    r = comm_alloc_local(cs[i]);
+  }
   for (int i = 0; i < nranks && r == mccsSuccess; ++i)
     for (int j = 0; j < nranks && r == mccsSuccess; ++j) r = enable_peer(devices[i], devices[j]);
   if (r == mccsSuccess) {
@@ -270,11 +295,15 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
       cs[i]->fifo_release = release;
       cs[i]->direct_ok = atomics;
     }
-    for (int i = 0; i < nranks && r == mccsSuccess; ++i) r = comm_build_device(cs[i]);
+    for (int i = 0; i < nranks && r == mccsSuccess; ++i) {
+      StepScope st("rank " + std::to_string(i));
+      r = comm_build_device(cs[i]);
+    }
     // node gate: one process sees every rank, so the host combines their verdicts
     bool distinct = false;
     for (int i = 1; i < nranks; ++i) distinct = distinct || devices[i] != devices[0];
     if (r == mccsSuccess && nranks > 1 && gate_wanted(distinct)) {
+      StepScope st("node gate");
       std::vector<bool> atomics_ok(nranks, atomics);
       r = comm_gate(cs, atomics_ok);
     }
@@ -299,28 +328,34 @@ static bool same_gpu(const ConnectHandle& a, const ConnectHandle& b) {
 
 extern "C" size_t mccsConnectHandleSize(void) { return sizeof(ConnectHandle); }
 
+// Exports the comm's FIFO arena for its peers.  An uncached arena whose
+// export is refused falls back to a plain device arena (system fences).
+static mccsResult_t export_arena(Comm* c, hipIpcMemHandle_t* h) {
+  StepScope st("IPC export of the FIFO arena");
+  DeviceGuard g(c->device);
+  hipError_t e = rt().IpcGetMemHandle(h, c->own_arena);
+  if (e == hipSuccess || !c->own_arena_uncached) {
+    MCCS_HIP(e);
+    return mccsSuccess;
+  }
+  MCCS_LOG("hipIpcGetMemHandle(uncached arena): %s; retrying with hipMalloc", hipGetErrorString(e));
+  MCCS_CHECK(comm_switch_to_device_arena(c));
+  MCCS_HIP(rt().IpcGetMemHandle(h, c->own_arena));
+  return mccsSuccess;
+}
+
 extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks, int device, const mccsCommConfig* cfg,
                                           void* handle_out) {
-  if (!out || !handle_out) return mccsInvalidArgument;
+  err_clear();
+  StepScope st0("mccsCommSetupRank(rank " + std::to_string(rank) + "/" + std::to_string(nranks) + ", device " +
+                std::to_string(device) + ")");
+  if (!out || !handle_out) MCCS_FAIL(mccsInvalidArgument, "null comm or handle pointer");
   Comm* c = nullptr;
   MCCS_CHECK(make_comm(rank, nranks, device, cfg, &c));
-  mccsResult_t r = comm_alloc_local(c);
   ConnectHandle h;
   std::memset(&h, 0, sizeof(h));
-  if (r == mccsSuccess) {
-    DeviceGuard g(device);
-    hipError_t e = hipIpcGetMemHandle(&h.ipc, c->own_arena);
-    if (e != hipSuccess && c->own_arena_uncached) {
-      // IPC export of the uncached arena refused: fall back to a plain device arena
-      MCCS_LOG("hipIpcGetMemHandle(uncached arena): %s; retrying with hipMalloc", hipGetErrorString(e));
-      (void)hipGetLastError();
-      if (comm_switch_to_device_arena(c) == mccsSuccess) e = hipIpcGetMemHandle(&h.ipc, c->own_arena);
-    }
-    if (e != hipSuccess) {
-      MCCS_LOG("hipIpcGetMemHandle: %s", hipGetErrorString(e));
-      r = mccsUnhandledCudaError;
-    }
-  }
+  mccsResult_t r = comm_alloc_local(c);
+  if (r == mccsSuccess) r = export_arena(c, &h.ipc);
   if (r != mccsSuccess) {
     comm_free(c);
     delete c;
@@ -347,38 +382,64 @@ extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks,
   h.slice_steps = c->slice_steps;
   h.block_threads = c->block_threads;
   h.gate_env = gate_env();
-  if (hipDeviceGetPCIBusId(h.pci, sizeof(h.pci) - 1, device) != hipSuccess) {
-    (void)hipGetLastError();
+  if (rt().DeviceGetPCIBusId(h.pci, sizeof(h.pci) - 1, device) != hipSuccess)
     std::snprintf(h.pci, sizeof(h.pci), "ordinal:%d", device);
-  }
   gethostname(h.host, sizeof(h.host) - 1);
   std::memcpy(handle_out, &h, sizeof(h));
   *out = (mccsComm_t)c;
   return mccsSuccess;
 }
 
+// Why rank r's handle cannot join this communicator ("" if it can).
+static std::string handle_mismatch(const Comm* c, const ConnectHandle& h, const ConnectHandle& mine, int r) {
+  char b[200];
+  auto diff = [&](const char* what, long long theirs, long long ours) {
+    std::snprintf(b, sizeof(b), "rank %d's %s %lld differs from this rank's %lld", r, what, theirs, ours);
+    return std::string(b);
+  };
+  if (h.magic != kHandleMagic) return "rank " + std::to_string(r) + "'s handle is not a connect handle";
+  if (h.rank != r) return diff("handle rank", h.rank, r);
+  if (h.nranks != c->nranks) return diff("nranks", h.nranks, c->nranks);
+  if (h.nch != c->nch) return diff("channel count", h.nch, c->nch);
+  if (h.arena_bytes != c->layout.total()) return diff("arena bytes", (long long)h.arena_bytes, (long long)c->layout.total());
+  if (h.buffer_size != c->layout.buffer_size) return diff("buffer_size", (long long)h.buffer_size, (long long)c->layout.buffer_size);
+  // ... or on which kernel / slice shape a call takes (both ends of every
+  // connection must run the same one: ADVICE r03)
+  if (h.direct_bytes != c->cfg.direct_bytes) return diff("direct_bytes", h.direct_bytes, c->cfg.direct_bytes);
+  if (h.oneshot_bytes != c->cfg.oneshot_bytes) return diff("oneshot_bytes", h.oneshot_bytes, c->cfg.oneshot_bytes);
+  if (h.ll_bytes != c->cfg.ll_bytes) return diff("ll_bytes", h.ll_bytes, c->cfg.ll_bytes);
+  if (h.fifo_slots != c->cfg.fifo_slots) return diff("fifo_slots", h.fifo_slots, c->cfg.fifo_slots);
+  if (h.slice_steps != c->slice_steps) return diff("slice steps", h.slice_steps, c->slice_steps);
+  if (h.block_threads != c->block_threads) return diff("block_threads", h.block_threads, c->block_threads);
+  // the node gate's collectives need every rank (a rank that skipped it
+  // would leave the others in its vote until the watchdog)
+  if (h.gate_env != mine.gate_env) return diff("MCCS_GATE", h.gate_env, mine.gate_env);
+  return "";
+}
+
 extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles) {
+  err_clear();
   Comm* c = (Comm*)comm;
-  if (!c || !all_handles || c->connected) return mccsInvalidUsage;
+  if (!c || !all_handles || c->connected) {
+    StepScope st0("mccsCommConnect");
+    MCCS_FAIL(mccsInvalidUsage, "null comm or handles, or the comm is already connected");
+  }
+  StepScope st0("mccsCommConnect(rank " + std::to_string(c->rank) + "/" + std::to_string(c->nranks) + ")");
   const ConnectHandle* hs = (const ConnectHandle*)all_handles;
   bool all_uc = true, release = false;
-  for (int r = 0; r < c->nranks; ++r) {
-    const ConnectHandle& h = hs[r];
-    if (h.magic != kHandleMagic || h.rank != r || h.nranks != c->nranks || h.nch != c->nch ||
-        h.arena_bytes != c->layout.total() || h.buffer_size != c->layout.buffer_size)
-      return mccsInvalidArgument;  // ranks disagree on the communicator profile
-    // ... or on which kernel / slice shape a call takes (both ends of every
-    // connection must run the same one: ADVICE r03)
-    if (h.direct_bytes != c->cfg.direct_bytes || h.oneshot_bytes != c->cfg.oneshot_bytes ||
-        h.ll_bytes != c->cfg.ll_bytes || h.fifo_slots != c->cfg.fifo_slots || h.slice_steps != c->slice_steps ||
-        h.block_threads != c->block_threads)
-      return mccsInvalidArgument;
-    // the node gate's collectives need every rank (a rank that skipped it
-    // would leave the others in its vote until the watchdog)
-    if (h.gate_env != hs[c->rank].gate_env) return mccsInvalidArgument;
-    all_uc = all_uc && h.fifo_memory != MCCS_FIFO_DEVICE;
-    release = release || h.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
-    if (h.lanes != hs[0].lanes || h.lanes_auto != hs[0].lanes_auto) return mccsInvalidArgument;
+  {
+    StepScope st("handle check");
+    for (int r = 0; r < c->nranks; ++r) {
+      const ConnectHandle& h = hs[r];
+      const std::string why = handle_mismatch(c, h, hs[c->rank], r);
+      // ranks disagree on the communicator profile
+      if (!why.empty()) MCCS_FAIL(mccsInvalidArgument, "%s", why.c_str());
+      all_uc = all_uc && h.fifo_memory != MCCS_FIFO_DEVICE;
+      release = release || h.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
+      if (h.lanes != hs[0].lanes || h.lanes_auto != hs[0].lanes_auto)
+        MCCS_FAIL(mccsInvalidArgument, "rank %d's lanes %d (auto %d) differ from rank 0's %d (auto %d)", r, h.lanes,
+                  h.lanes_auto, hs[0].lanes, hs[0].lanes_auto);
+    }
   }
   // Ranks of this communicator that share a GPU as separate processes run
   // separate launches that spin on each other's flags, so all of them must be
@@ -389,6 +450,7 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
   // refused instead of deadlocking.  Every rank derives the same lane count
   // from the same handles (a connection's two ends must agree on lanes).
   {
+    StepScope st("co-residency");
     int max_share = 1, cap = 1 << 30;
     for (int r = 0; r < c->nranks; ++r) {
       int share = 0;
@@ -400,27 +462,29 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
     if (max_share > 1 && cap < (1 << 30)) {
       if (hs[0].lanes_auto) {
         const int fit = cap / 2 / (max_share * c->nch);
-        if (fit < 1) return mccsInvalidUsage;
+        if (fit < 1)
+          MCCS_FAIL(mccsInvalidUsage, "%d ranks x %d channels per GPU do not fit half of %d workgroup slots", max_share,
+                    c->nch, cap);
         c->lanes = std::min(c->lanes, fit);
       } else if ((long)max_share * c->nch * c->lanes > cap) {
-        return mccsInvalidUsage;
+        MCCS_FAIL(mccsInvalidUsage, "%d ranks x %d channels x %d lanes per GPU exceed %d workgroup slots", max_share,
+                  c->nch, c->lanes, cap);
       }
     }
   }
   DeviceGuard g(c->device);
   for (int r = 0; r < c->nranks; ++r) {
     if (r == c->rank) continue;
+    StepScope st("IPC open of rank " + std::to_string(r) + "'s arena");
     const ConnectHandle& h = hs[r];
-    if (h.pid == (int32_t)getpid()) return mccsInvalidUsage;  // same process: use mccsCommInitAll
-    int peer_dev = -1;                                         // the peer's GPU as this process numbers it
-    if (hipDeviceGetByPCIBusId(&peer_dev, h.pci) != hipSuccess) (void)hipGetLastError();
-    if (peer_dev >= 0) (void)enable_peer(c->device, peer_dev);  // best effort; IPC maps regardless
+    if (h.pid == (int32_t)getpid())  // same process: use mccsCommInitAll
+      MCCS_FAIL(mccsInvalidUsage, "rank %d is in this process (pid %d): use mccsCommInitAll", r, (int)h.pid);
+    int peer_dev = -1;  // the peer's GPU as this process numbers it
+    if (rt().DeviceGetByPCIBusId(&peer_dev, h.pci) != hipSuccess) peer_dev = -1;
+    if (peer_dev >= 0 && enable_peer(c->device, peer_dev) != mccsSuccess)
+      err_clear();  // best effort; IPC maps regardless
     void* p = nullptr;
-    hipError_t e = hipIpcOpenMemHandle(&p, h.ipc, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) {
-      MCCS_LOG("hipIpcOpenMemHandle(rank %d): %s", r, hipGetErrorString(e));
-      return mccsUnhandledCudaError;
-    }
+    MCCS_HIP(rt().IpcOpenMemHandle(&p, h.ipc));
     c->peer_arena[r] = (char*)p;
     c->peer_opened_ipc[r] = true;
   }
@@ -435,17 +499,16 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
     if (same_gpu(hs[r], hs[c->rank])) continue;
     distinct = true;
     int dev = -1, ok = 0;
-    if (hipDeviceGetByPCIBusId(&dev, hs[r].pci) != hipSuccess || dev < 0) {
-      (void)hipGetLastError();
-      atomics = false;
-    } else if (rt().P2PAtomics(&ok, c->device, dev) != hipSuccess || !ok) {
-      (void)hipGetLastError();
-      atomics = false;
-    }
+    if (rt().DeviceGetByPCIBusId(&dev, hs[r].pci) != hipSuccess || dev < 0) atomics = false;
+    else if (rt().P2PAtomics(&ok, c->device, dev) != hipSuccess || !ok) atomics = false;
   }
   c->direct_ok = atomics;
-  MCCS_CHECK(comm_build_device(c));
+  {
+    StepScope st("device structures");
+    MCCS_CHECK(comm_build_device(c));
+  }
   if (gate_wanted(distinct)) {
+    StepScope st("node gate");
     std::vector<Comm*> cs{c};
     mccsResult_t r = comm_gate(cs, std::vector<bool>{atomics});
     if (r != mccsSuccess) {
@@ -476,6 +539,7 @@ extern "C" mccsResult_t mccsGroupStart(void) {
 }
 
 extern "C" mccsResult_t mccsGroupEnd(void) {
+  err_clear();
   if (g_group.depth <= 0) return mccsInvalidUsage;
   if (--g_group.depth > 0) return mccsSuccess;
   if (g_group.error != mccsSuccess) {  // a collective of the group was rejected: launch none
@@ -490,6 +554,8 @@ extern "C" mccsResult_t mccsGroupEnd(void) {
 }
 
 extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
+  err_clear();
+  StepScope st0("mccsCommSync");
   Comm* c = (Comm*)comm;
   if (!c) return mccsInvalidArgument;
   DeviceGuard g(c->device);
@@ -505,8 +571,10 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
   MCCS_HIP(rt().Memcpy(line, c->d_abort, sizeof(line), hipMemcpyDeviceToHost));
   const uint32_t abort_val = line[0], err = line[1];
   if (err || abort_val) c->failed = true;
-  if (err & MCCS_ERR_TIMEOUT) return mccsTimeout;
-  if (err || abort_val) return mccsRemoteError;
+  if (err & MCCS_ERR_TIMEOUT)
+    MCCS_FAIL(mccsTimeout, "rank %d: a FIFO wait passed the %d ms watchdog (error bits 0x%x)", c->rank,
+              c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms, err);
+  if (err || abort_val) MCCS_FAIL(mccsRemoteError, "rank %d: abortFlag %u, error bits 0x%x", c->rank, abort_val, err);
   return mccsSuccess;
 }
 

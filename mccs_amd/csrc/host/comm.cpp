@@ -10,6 +10,7 @@
 // connection and the head/tail flag lines; peers reach it over xGMI through
 // peer access (same process) or IPC (one rank per process).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -107,10 +108,7 @@ bool devices_p2p_atomics(const std::vector<int>& devices) {
   for (int a : devices)
     for (int b : devices) {
       int ok = 0;
-      if (rt().P2PAtomics(&ok, a, b) != hipSuccess || !ok) {
-        (void)hipGetLastError();
-        return false;
-      }
+      if (rt().P2PAtomics(&ok, a, b) != hipSuccess || !ok) return false;
     }
   return true;
 }
@@ -178,6 +176,13 @@ void comm_pool_drop_generation(unsigned generation) {
     else ++i;
 }
 
+int comm_pool_count(unsigned generation) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  int n = 0;
+  for (const auto& a : g_pool) n += a.generation == generation;
+  return n;
+}
+
 // Live communicators' device structures -> their FIFO depth, so the external
 // launch (mccs_hip_launch_coll, whose reference-named kernels assume the
 // reference's 8 slots) can refuse a library communicator built with another.
@@ -194,6 +199,7 @@ int comm_fifo_slots_of(const void* d_comm) {
 // Swap this comm's uncached arena for a plain device arena (used when IPC
 // export of the uncached one is refused).  The old range goes back to the pool.
 mccsResult_t comm_switch_to_device_arena(Comm* c) {
+  StepScope st("device arena fallback");
   DeviceGuard g(c->device);
   const size_t bytes = c->layout.total();
   if (c->own_arena) pool_give(c->device, c->own_arena_uncached, bytes, c->own_arena);
@@ -208,6 +214,7 @@ mccsResult_t comm_switch_to_device_arena(Comm* c) {
 }
 
 mccsResult_t comm_alloc_local(Comm* c) {
+  StepScope st0("comm_alloc_local");
   DeviceGuard g(c->device);
   c->layout.nch = c->nch;
   c->layout.buffer_size = (size_t)c->cfg.buffer_size;
@@ -224,69 +231,89 @@ mccsResult_t comm_alloc_local(Comm* c) {
   const size_t bytes = c->layout.total();
   c->own_arena = nullptr;
   c->own_arena_uncached = false;
-  if (c->cfg.fifo_memory != MCCS_FIFO_DEVICE) {  // UNCACHED or UNCACHED_RELEASE
-    c->own_arena = pool_take(c->device, true, bytes);
-    if (c->own_arena) {
-      c->own_arena_uncached = true;
-    } else {
-      hipError_t e = rt().MallocUncached((void**)&c->own_arena, bytes);
-      if (e == hipSuccess) {
-        c->own_arena_uncached = true;
-      } else {
-        (void)hipGetLastError();
-        MCCS_LOG("uncached FIFO arena unavailable (%s); using hipMalloc + system fences", hipGetErrorString(e));
-        c->own_arena = nullptr;
-      }
-    }
-  }
-  if (!c->own_arena) {
-    c->own_arena = pool_take(c->device, false, bytes);
-    if (!c->own_arena) MCCS_HIP(rt().Malloc((void**)&c->own_arena, bytes));
-  }
-  // trust but verify: the runtime must report the uncached allocation flag
-  if (c->own_arena_uncached && !rt().IsUncached(c->own_arena)) {
-    MCCS_LOG("arena %p is not reported uncached: using system fences", (void*)c->own_arena);
-    c->own_arena_uncached = false;
-  }
-  if (std::getenv("MCCS_DEBUG"))
-    MCCS_LOG("rank %d arena %p bytes %zu uncached=%d", c->rank, (void*)c->own_arena, bytes,
-             (int)c->own_arena_uncached);
-  MCCS_HIP(rt().Memset(c->own_arena, 0, bytes));
-  MCCS_HIP(rt().FlushCaches());
-  MCCS_HIP(rt().DeviceSynchronize());
+  // the peer tables first: comm_free may run after any step below fails
   c->peer_arena.assign(c->nranks, nullptr);
   c->peer_opened_ipc.assign(c->nranks, false);
-  c->peer_arena[c->rank] = c->own_arena;
-
-  MCCS_HIP(rt().Malloc((void**)&c->d_abort, 64));
-  MCCS_HIP(rt().Memset(c->d_abort, 0, 64));  // the reference leaves it uninitialised (device.rs:157)
-  MCCS_HIP(rt().Malloc((void**)&c->d_comm,
-                       sizeof(mccsDevCommAndChannels) + sizeof(mccsRingConnView) * MCCS_MAX_NCHANNELS));
-  c->d_view = (mccsRingConnView*)((char*)c->d_comm + sizeof(mccsDevCommAndChannels));
   c->d_peers.assign(c->nch, nullptr);
   c->d_user_ranks.assign(c->nch, nullptr);
-  for (int ch = 0; ch < c->nch; ++ch) {
-    MCCS_HIP(rt().Malloc((void**)&c->d_peers[ch], sizeof(mccsDevChannelPeer) * c->nranks));
-    MCCS_HIP(rt().Malloc((void**)&c->d_user_ranks[ch], sizeof(int) * c->nranks));
+  {
+    StepScope st("FIFO arena");
+    if (c->cfg.fifo_memory != MCCS_FIFO_DEVICE) {  // UNCACHED or UNCACHED_RELEASE
+      c->own_arena = pool_take(c->device, true, bytes);
+      if (c->own_arena) {
+        c->own_arena_uncached = true;
+      } else {
+        hipError_t e = rt().MallocUncached((void**)&c->own_arena, bytes);
+        if (e == hipSuccess) {
+          c->own_arena_uncached = true;
+        } else {
+          MCCS_LOG("uncached FIFO arena unavailable (%s); using hipMalloc + system fences", hipGetErrorString(e));
+          c->own_arena = nullptr;
+        }
+      }
+    }
+    if (!c->own_arena) {
+      c->own_arena = pool_take(c->device, false, bytes);
+      if (!c->own_arena) MCCS_HIP(rt().Malloc((void**)&c->own_arena, bytes));
+    }
+    // trust but verify: the runtime must report the uncached allocation flag
+    if (c->own_arena_uncached && !rt().IsUncached(c->own_arena)) {
+      MCCS_LOG("arena %p is not reported uncached: using system fences", (void*)c->own_arena);
+      c->own_arena_uncached = false;
+    }
+    if (std::getenv("MCCS_DEBUG"))
+      MCCS_LOG("rank %d arena %p bytes %zu uncached=%d", c->rank, (void*)c->own_arena, bytes,
+               (int)c->own_arena_uncached);
+    c->peer_arena[c->rank] = c->own_arena;
   }
-  c->work_depth = (uint32_t)c->cfg.work_fifo_depth;
-  MCCS_HIP(rt().HostMallocMapped((void**)&c->h_work, sizeof(mccsDevWork) * c->work_depth));
-  MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_work, c->h_work));
-  std::memset(c->h_work, 0, sizeof(mccsDevWork) * c->work_depth);
-  MCCS_HIP(rt().HostMallocMapped((void**)&c->h_graph_work, sizeof(mccsDevWork) * Comm::kGraphWorkEntries));
-  MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_graph_work, c->h_graph_work));
-  std::memset(c->h_graph_work, 0, sizeof(mccsDevWork) * Comm::kGraphWorkEntries);
-  c->graph_work_used = 0;
-  MCCS_HIP(rt().HostMallocMapped((void**)&c->h_done, sizeof(uint32_t) * MCCS_MAX_NCHANNELS));
-  MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_done, c->h_done));
-  std::memset(c->h_done, 0, sizeof(uint32_t) * MCCS_MAX_NCHANNELS);
+  {
+    StepScope st("FIFO arena zero-fill");
+    MCCS_HIP(rt().Memset(c->own_arena, 0, bytes));
+    MCCS_HIP(rt().FlushCaches());
+    MCCS_HIP(rt().DeviceSynchronize());
+  }
+  {
+    StepScope st("device comm");
+    MCCS_HIP(rt().Malloc((void**)&c->d_abort, 64));
+    MCCS_HIP(rt().Memset(c->d_abort, 0, 64));  // the reference leaves it uninitialised (device.rs:157)
+    MCCS_HIP(rt().Malloc((void**)&c->d_comm,
+                         sizeof(mccsDevCommAndChannels) + sizeof(mccsRingConnView) * MCCS_MAX_NCHANNELS));
+    c->d_view = (mccsRingConnView*)((char*)c->d_comm + sizeof(mccsDevCommAndChannels));
+    for (int ch = 0; ch < c->nch; ++ch) {
+      MCCS_HIP(rt().Malloc((void**)&c->d_peers[ch], sizeof(mccsDevChannelPeer) * c->nranks));
+      MCCS_HIP(rt().Malloc((void**)&c->d_user_ranks[ch], sizeof(int) * c->nranks));
+    }
+  }
+  {
+    StepScope st("work FIFO");
+    c->work_depth = (uint32_t)c->cfg.work_fifo_depth;
+    MCCS_HIP(rt().HostMallocMapped((void**)&c->h_work, sizeof(mccsDevWork) * c->work_depth));
+    MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_work, c->h_work));
+    std::memset(c->h_work, 0, sizeof(mccsDevWork) * c->work_depth);
+  }
+  {
+    StepScope st("graph work arena");
+    MCCS_HIP(rt().HostMallocMapped((void**)&c->h_graph_work, sizeof(mccsDevWork) * Comm::kGraphWorkEntries));
+    MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_graph_work, c->h_graph_work));
+    std::memset(c->h_graph_work, 0, sizeof(mccsDevWork) * Comm::kGraphWorkEntries);
+    c->graph_work_used = 0;
+  }
+  {
+    StepScope st("work done counters");
+    MCCS_HIP(rt().HostMallocMapped((void**)&c->h_done, sizeof(uint32_t) * MCCS_MAX_NCHANNELS));
+    MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_done, c->h_done));
+    std::memset(c->h_done, 0, sizeof(uint32_t) * MCCS_MAX_NCHANNELS);
+  }
   c->chan_next.assign(c->nch, 0);
   c->work_next = 0;
   c->work_acked_min = 0;
-  // comm stream: created on first use (comm_stream); the event becomes
-  // interprocess only when a backend exports it (comm_make_event_ipc)
-  MCCS_HIP(rt().EventCreate(&c->event, hipEventDisableTiming));
-  MCCS_HIP(rt().EventCreate(&c->user_event, hipEventDisableTiming));
+  {
+    // comm stream: created on first use (comm_stream); the event becomes
+    // interprocess only when a backend exports it (comm_make_event_ipc)
+    StepScope st("events");
+    MCCS_HIP(rt().EventCreate(&c->event, hipEventDisableTiming));
+    MCCS_HIP(rt().EventCreate(&c->user_event, hipEventDisableTiming));
+  }
   c->sched.assign(c->nch, ChannelSchedule{});
   return mccsSuccess;
 }
@@ -318,7 +345,7 @@ mccsResult_t comm_build_device(Comm* c) {
       char* me = c->peer_arena[c->rank];
       char* nx = c->peer_arena[next];
       char* pv = c->peer_arena[prev];
-      if (!me || !nx || !pv) return mccsInternalError;
+      if (!me || !nx || !pv) MCCS_FAIL(mccsInternalError, "channel %d: a neighbour's FIFO arena is not mapped", ch);
       const ArenaLayout& L = c->layout;
       // send connector (to next): poll our head lines, post next's tail lines
       mccsDevConnInfo& s = peers[next].send[0];
@@ -366,26 +393,49 @@ mccsResult_t comm_stream(Comm* c, hipStream_t* out) {
 // InitCommunicator's event handle (libmccs communicator.rs:35-38): a backend
 // process exports the comm event to the application, so it must be an
 // interprocess event.  Pending work is drained first, so the new event is
-// recorded after every later launch and no earlier one is lost.
+// recorded after every later launch and no earlier one is lost.  Fused comms
+// whose launches this comm's event tracked read it through sync_owner at wait
+// time, so they see the new one; the old one is destroyed once no thread
+// synchronizes on it.
 mccsResult_t comm_make_event_ipc(Comm* c) {
   if (c->event_ipc) return mccsSuccess;
+  StepScope st("interprocess comm event");
   DeviceGuard g(c->device);
-  if (c->event_recorded) MCCS_HIP(hipEventSynchronize(c->event));
-  else MCCS_HIP(hipDeviceSynchronize());  // the latest launches recorded no event
+  if (c->event_recorded) MCCS_HIP(rt().EventSynchronize(c->event));
+  else MCCS_HIP(rt().DeviceSynchronize());  // the latest launches recorded no event
   hipEvent_t e = nullptr;
-  MCCS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess));
-  (void)hipEventDestroy(c->event);
-  c->event = e;
+  MCCS_HIP(rt().EventCreate(&e, hipEventDisableTiming | hipEventInterprocess));
+  hipEvent_t old;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    old = c->event;
+    c->event = e;
+  }
+  while (c->waiters.load() > 0) sched_yield();
+  (void)rt().EventDestroy(old);
   c->event_ipc = true;
   return mccsSuccess;
 }
 
 hipError_t comm_wait_last_launch(Comm* c) {
   if (c->event_recorded) return rt().EventSynchronize(c->event);
+  Comm* owner = nullptr;
+  hipEvent_t ev = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_live_mu);
-    if (c->sync_event && c->sync_owner && g_live_comms.count(const_cast<Comm*>(c->sync_owner)))
-      return rt().EventSynchronize(c->sync_event);
+    if (c->sync_owner && g_live_comms.count(c->sync_owner)) {
+      owner = c->sync_owner;
+      ev = owner->event;
+      owner->waiters.fetch_add(1);
+    }
+  }
+  if (owner) {
+    // Outside the lock: a kernel spinning on its peers can keep
+    // this wait going until the watchdog, and the lock guards every launch's
+    // FIFO-depth lookup and every comm's build and free.
+    const hipError_t e = rt().EventSynchronize(ev);
+    owner->waiters.fetch_sub(1);
+    return e;
   }
   return rt().DeviceSynchronize();  // nothing recorded the launch: every stream of the device
 }
@@ -399,17 +449,17 @@ mccsResult_t comm_free(Comm* c) {
     g_live_fifo_slots.erase(c->d_comm);
     g_live_comms.erase(c);
     for (Comm* x : g_live_comms)
-      if (x->sync_owner == c) {
-        x->sync_owner = nullptr;
-        x->sync_event = nullptr;
-      }
+      if (x->sync_owner == c) x->sync_owner = nullptr;
   }
+  while (c->waiters.load() > 0) sched_yield();  // a fused comm's wait on our event
   if (c->stream) (void)rt().StreamSynchronize(c->stream);
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
-    if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)hipIpcCloseMemHandle(c->peer_arena[r]);
+    if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)rt().IpcCloseMemHandle(c->peer_arena[r]);
   if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->layout.total(), c->own_arena);
-  for (auto p : c->d_peers) (void)rt().Free(p);
-  for (auto p : c->d_user_ranks) (void)rt().Free(p);
+  for (auto p : c->d_peers)
+    if (p) (void)rt().Free(p);
+  for (auto p : c->d_user_ranks)
+    if (p) (void)rt().Free(p);
   if (c->d_comm) (void)rt().Free(c->d_comm);
   if (c->d_abort) (void)rt().Free(c->d_abort);
   if (c->h_work) (void)rt().HostFree(c->h_work);

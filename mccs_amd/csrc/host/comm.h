@@ -10,6 +10,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -28,14 +29,37 @@ namespace mccs {
     std::fprintf(stderr, "\n");              \
   } while (0)
 
-// cuda_warning! equivalent (utils/mod.rs:7-26): log, then fail the call.
-#define MCCS_HIP(call)                                                                    \
-  do {                                                                                    \
-    hipError_t _e = (call);                                                               \
-    if (_e != hipSuccess) {                                                               \
-      MCCS_LOG("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(_e));       \
-      return mccsUnhandledCudaError;                                                      \
-    }                                                                                     \
+// ---- failure diagnosis (diag.cpp; mccsGetLastErrorString) -----------------
+// A failing library call records, on the calling thread, the step it failed
+// in (the stack of StepScope names open at the failure), the failing runtime
+// call and its hipError_t.  The reference logs a CUDA failure and returns one
+// code (cuda_warning!, utils/mod.rs:7-26); this keeps the same one code and
+// adds where and why.
+struct StepScope {
+  explicit StepScope(std::string name);
+  ~StepScope();
+  StepScope(const StepScope&) = delete;
+  StepScope& operator=(const StepScope&) = delete;
+};
+void err_clear();                                                    // at each API entry
+void err_hip(const char* call, hipError_t e, const char* file, int line);  // a HIP / rt() call failed
+void err_note(const char* file, int line, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+
+// cuda_warning! equivalent (utils/mod.rs:7-26): record + log, then fail the call.
+#define MCCS_HIP(call)                                  \
+  do {                                                  \
+    hipError_t _e = (call);                             \
+    if (_e != hipSuccess) {                             \
+      ::mccs::err_hip(#call, _e, __FILE__, __LINE__);   \
+      return mccsUnhandledCudaError;                    \
+    }                                                   \
+  } while (0)
+
+// A refused call (bad argument, mismatched peers): record why, then fail.
+#define MCCS_FAIL(code, ...)                              \
+  do {                                                    \
+    ::mccs::err_note(__FILE__, __LINE__, __VA_ARGS__);    \
+    return (code);                                        \
   } while (0)
 
 #define MCCS_CHECK(call)                  \
@@ -182,8 +206,12 @@ struct Comm {
   // event, so mccsCommSync waits on this launch and not on the whole device
   // (a device-wide wait would also wait on other communicators' kernels that
   // spin on their peers: ADVICE r03).  Cleared when the owner is freed.
-  hipEvent_t sync_event = nullptr;
-  const Comm* sync_owner = nullptr;
+  // The owner's event is read at wait time (under the live-comm lock), so an
+  // owner that replaces its event (comm_make_event_ipc) leaves no dangling copy.
+  Comm* sync_owner = nullptr;
+  // Threads synchronizing on this comm's event outside the live-comm lock
+  // (comm_wait_last_launch): the event is not destroyed or replaced while > 0.
+  std::atomic<int> waiters{0};
   hipEvent_t user_event = nullptr;  // user -> comm
   bool connected = false;
   bool failed = false;
@@ -228,6 +256,7 @@ mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream
 mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one
 int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live library comm's device struct, else 0
 void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
+int comm_pool_count(unsigned generation);             // arenas pooled under that runtime (tests)
 // gate.cpp
 bool gate_wanted(bool distinct_gpus);
 int gate_env();  // MCCS_GATE: -1 unset, else its value

@@ -23,7 +23,9 @@
 // device ordinals that are local to its process).  A direct test launch that
 // hits the (5 s) watchdog counts as a wrong sum for that variant; a ring
 // launch that does fails the connect with mccsTimeout (a hang leaves the
-// ranks' FIFO steps out of step, which no local reset repairs).
+// ranks' FIFO steps out of step, which no local reset repairs).  Across
+// processes the ranks first meet in one ring launch under the configured
+// watchdog (gate_barrier), so a peer that enters Connect late is waited for.
 //
 // MCCS_GATE=0 skips the gate; MCCS_GATE=1 runs it even when every rank is on
 // one GPU (tests).  Test seams, honoured only with MCCS_TEST_HOOKS=1:
@@ -196,6 +198,10 @@ mccsResult_t gate_allreduce(std::vector<Comm*>& cs, std::vector<Buf>& bufs, size
 // are reported wrong (the vote turns them off on every rank).
 mccsResult_t gate_path(std::vector<Comm*>& cs, std::vector<Buf>& bufs, unsigned bit, std::vector<unsigned>* fail,
                        bool* direct_dead) {
+  StepScope st(bit == MCCS_GATE_LL        ? "LL test"
+               : bit == MCCS_GATE_ONESHOT ? "one-shot test"
+               : bit == MCCS_GATE_TWOSHOT ? "two-shot test"
+                                          : "ring test (hand-off " + std::to_string(cs[0]->kcfg.fence_mode) + ")");
   constexpr unsigned kDirect = MCCS_GATE_LL | MCCS_GATE_ONESHOT | MCCS_GATE_TWOSHOT;
   const bool direct = bit & kDirect;
   bool skip = direct && *direct_dead;
@@ -228,46 +234,69 @@ mccsResult_t gate_path(std::vector<Comm*>& cs, std::vector<Buf>& bufs, unsigned 
   return mccsSuccess;
 }
 
+// One ring AllReduce(MAX) of kVoteWords uint32 (in/out `v`) over this
+// process's one rank of the communicator, in the cached mode with
+// system-scope fences (the reference's hand-off) whatever mode is configured,
+// under a watchdog of `ticks` (0: none).
+constexpr int kVoteWords = 32;
+mccsResult_t ring_max(Comm* c, Buf& b, uint32_t* v, uint64_t ticks) {
+  DeviceGuard g(c->device);
+  MCCS_HIP(rt().Memcpy(b.send, v, kVoteWords * 4, hipMemcpyHostToDevice));
+  Route route(c, 0);
+  const mccsRingKernelCfg saved = c->kcfg;
+  c->kcfg.fence_mode = MCCS_FENCE_SYSTEM;
+  c->kcfg.timeout_ticks = ticks;
+  mccsResult_t r = mccsAllReduce(b.send, b.recv, kVoteWords, mccsUint32, mccsDevMax, (mccsComm_t)c, nullptr);
+  if (r == mccsSuccess) r = mccsCommSync((mccsComm_t)c);
+  c->kcfg = saved;
+  MCCS_CHECK(r);
+  MCCS_HIP(rt().Memcpy(v, b.recv, kVoteWords * 4, hipMemcpyDeviceToHost));
+  return mccsSuccess;
+}
+
 // Every rank's failure bits ORed, the same answer on every rank.  In one
 // process: the host ORs them.  Across processes (cs.size() == 1 < nranks):
-// one ring AllReduce(MAX) over one uint32 per bit, run in the cached mode with
-// system-scope fences (the reference's hand-off) whatever mode is configured.
+// one ring_max over one uint32 per bit.
 mccsResult_t gate_vote(std::vector<Comm*>& cs, std::vector<Buf>& bufs, std::vector<unsigned>* fail,
                        unsigned* agreed) {
+  StepScope st("vote");
   unsigned all = 0;
   for (unsigned f : *fail) all |= f;
   if ((int)cs.size() == cs[0]->nranks) {
     *agreed = all;
     return mccsSuccess;
   }
-  Comm* c = cs[0];
-  constexpr int kBits = 32;
-  uint32_t v[kBits];
-  for (int b = 0; b < kBits; ++b) v[b] = (all >> b) & 1u;
-  DeviceGuard g(c->device);
-  MCCS_HIP(rt().Memcpy(bufs[0].send, v, sizeof(v), hipMemcpyHostToDevice));
-  Route route(c, 0);
-  const mccsRingKernelCfg saved = c->kcfg;
-  c->kcfg.fence_mode = MCCS_FENCE_SYSTEM;
+  uint32_t v[kVoteWords];
+  for (int b = 0; b < kVoteWords; ++b) v[b] = (all >> b) & 1u;
   // a peer may still sit in a direct test launch until its own (5 s)
   // watchdog fires before this ring launch runs there: wait longer here
-  c->kcfg.timeout_ticks = 3ull * kGateTimeoutTicks;
-  mccsResult_t r = mccsAllReduce(bufs[0].send, bufs[0].recv, kBits, mccsUint32, mccsDevMax, (mccsComm_t)c, nullptr);
-  if (r == mccsSuccess) r = mccsCommSync((mccsComm_t)c);
-  c->kcfg = saved;
-  MCCS_CHECK(r);
-  MCCS_HIP(rt().Memcpy(v, bufs[0].recv, sizeof(v), hipMemcpyDeviceToHost));
+  MCCS_CHECK(ring_max(cs[0], bufs[0], v, 3ull * kGateTimeoutTicks));
   if (assume_pass()) {  // nothing ran: the local bits stand for the vote
     *agreed = all;
     return mccsSuccess;
   }
   unsigned out = 0;
-  for (int b = 0; b < kBits; ++b) {
-    if (v[b] > 1) return mccsInternalError;  // a vote that is not 0/1 came back corrupted
+  for (int b = 0; b < kVoteWords; ++b) {
+    // a vote that is not 0/1 came back corrupted
+    if (v[b] > 1) MCCS_FAIL(mccsInternalError, "vote word %d came back as %u", b, v[b]);
     out |= (v[b] & 1u) << b;
   }
   *agreed = out;
   return mccsSuccess;
+}
+
+// Across processes, the ranks enter Connect at different times (a peer still
+// loading code objects, opening IPC handles, or on a loaded host).  The
+// gate's test launches run under a 5 s watchdog counted from kernel start, so
+// before them the ranks meet in one ring launch under the communicator's own
+// watchdog (a peer 5 s late used to fail the connect with
+// mccsTimeout, or vote a direct variant off).  After it the ranks are in step
+// to within host jitter.  One fused launch (cs.size() == nranks) needs none.
+mccsResult_t gate_barrier(std::vector<Comm*>& cs, std::vector<Buf>& bufs, uint64_t configured_ticks) {
+  if ((int)cs.size() == cs[0]->nranks) return mccsSuccess;
+  StepScope st("barrier");
+  uint32_t v[kVoteWords] = {0};
+  return ring_max(cs[0], bufs[0], v, configured_ticks);
 }
 
 }  // namespace
@@ -296,8 +325,10 @@ mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_
   for (size_t k = 0; k < cs.size() && r == mccsSuccess; ++k) {
     DeviceGuard g(cs[k]->device);
     if (rt().Malloc((void**)&bufs[k].send, max_count * 4) != hipSuccess ||
-        rt().Malloc((void**)&bufs[k].recv, max_count * 4) != hipSuccess)
+        rt().Malloc((void**)&bufs[k].recv, max_count * 4) != hipSuccess) {
+      err_note(__FILE__, __LINE__, "test buffers: Malloc of %zu bytes failed", max_count * 4);
       r = mccsUnhandledCudaError;
+    }
     // a gate launch that hangs ends after 5 s, not the configured 30 s
     saved_ticks[k] = cs[k]->kcfg.timeout_ticks;
     if (saved_ticks[k] == 0 || saved_ticks[k] > kGateTimeoutTicks) cs[k]->kcfg.timeout_ticks = kGateTimeoutTicks;
@@ -308,6 +339,7 @@ mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_
   // peer atomics: a rank that cannot do them turns the count-based variants off everywhere
   for (size_t k = 0; k < cs.size(); ++k)
     if (!atomics_ok[k]) fail[k] |= MCCS_GATE_NO_ATOMICS;
+  if (r == mccsSuccess) r = gate_barrier(cs, bufs, saved_ticks[0]);
   // 1. the ring, stepping down the hand-off ladder until every rank's sums are exact
   for (int attempt = 0; attempt < 3 && r == mccsSuccess; ++attempt) {
     const unsigned bit = ring_bit(cs[0]->kcfg.fence_mode);
@@ -322,7 +354,7 @@ mccsResult_t comm_gate(std::vector<Comm*>& cs, const std::vector<bool>& atomics_
     if (!(agreed & bit)) break;
     failed |= bit;
     if (bit == MCCS_GATE_RING_SYSTEM) {
-      MCCS_LOG("node gate: the ring AllReduce is wrong in every hand-off mode; refusing the communicator");
+      err_note(__FILE__, __LINE__, "the ring AllReduce is wrong in every hand-off mode; refusing the communicator");
       r = mccsSystemError;
       break;
     }

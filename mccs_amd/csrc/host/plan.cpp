@@ -692,8 +692,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     for (size_t k = 0; k < idx.size(); ++k) {
       comms[idx[k]]->event_recorded = record;
       // fused rank slots without their own record wait on the launching comm's event
-      comms[idx[k]]->sync_event = (k > 0 && !record && stop_on_launch) ? c0->event : nullptr;
-      comms[idx[k]]->sync_owner = comms[idx[k]]->sync_event ? c0 : nullptr;
+      comms[idx[k]]->sync_owner = (k > 0 && !record && stop_on_launch) ? c0 : nullptr;
       comms[idx[k]]->last_algo = !direct                            ? MCCS_ALGO_RING
                                  : da.mode == MCCS_DIRECT_TWO_SHOT ? MCCS_ALGO_DIRECT
                                  : da.mode == MCCS_DIRECT_LL_ONE_SHOT || da.mode == MCCS_DIRECT_LL_AG ? MCCS_ALGO_LL

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -14,6 +15,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 
 #include "comm.h"
 
@@ -21,14 +23,23 @@ namespace mccs {
 
 namespace {
 
+// Every failing call's error is returned and also cleared from HIP's
+// per-thread last error: callers see it once, through the return value, and
+// no later hipGetLastError() (torch checks one after each of its kernel
+// launches) reports a failure of ours that was already handled.
 class HipRuntime final : public DeviceRuntime {
+  static hipError_t ret(hipError_t e) {
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e;
+  }
+
  public:
-  hipError_t GetDeviceCount(int* n) override { return hipGetDeviceCount(n); }
-  hipError_t GetDevice(int* d) override { return hipGetDevice(d); }
-  hipError_t SetDevice(int d) override { return hipSetDevice(d); }
-  hipError_t Malloc(void** p, size_t bytes) override { return hipMalloc(p, bytes); }
+  hipError_t GetDeviceCount(int* n) override { return ret(hipGetDeviceCount(n)); }
+  hipError_t GetDevice(int* d) override { return ret(hipGetDevice(d)); }
+  hipError_t SetDevice(int d) override { return ret(hipSetDevice(d)); }
+  hipError_t Malloc(void** p, size_t bytes) override { return ret(hipMalloc(p, bytes)); }
   hipError_t MallocUncached(void** p, size_t bytes) override {
-    return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    return ret(hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached));
   }
   bool IsUncached(void* p) override {
     hipPointerAttribute_t attr;
@@ -39,23 +50,23 @@ class HipRuntime final : public DeviceRuntime {
     }
     return attr.allocationFlags == hipDeviceMallocUncached;
   }
-  hipError_t Free(void* p) override { return hipFree(p); }
-  hipError_t Memset(void* p, int v, size_t bytes) override { return hipMemset(p, v, bytes); }
+  hipError_t Free(void* p) override { return ret(hipFree(p)); }
+  hipError_t Memset(void* p, int v, size_t bytes) override { return ret(hipMemset(p, v, bytes)); }
   hipError_t Memcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) override {
-    return hipMemcpy(dst, src, bytes, kind);
+    return ret(hipMemcpy(dst, src, bytes, kind));
   }
-  hipError_t HostMallocMapped(void** p, size_t bytes) override { return hipHostMalloc(p, bytes, hipHostMallocMapped); }
-  hipError_t HostGetDevicePointer(void** d, void* h) override { return hipHostGetDevicePointer(d, h, 0); }
-  hipError_t HostFree(void* p) override { return hipHostFree(p); }
-  hipError_t DeviceSynchronize() override { return hipDeviceSynchronize(); }
-  hipError_t FlushCaches() override { return ring_flush_caches(nullptr); }
-  hipError_t CanAccessPeer(int* can, int dev, int peer) override { return hipDeviceCanAccessPeer(can, dev, peer); }
+  hipError_t HostMallocMapped(void** p, size_t bytes) override { return ret(hipHostMalloc(p, bytes, hipHostMallocMapped)); }
+  hipError_t HostGetDevicePointer(void** d, void* h) override { return ret(hipHostGetDevicePointer(d, h, 0)); }
+  hipError_t HostFree(void* p) override { return ret(hipHostFree(p)); }
+  hipError_t DeviceSynchronize() override { return ret(hipDeviceSynchronize()); }
+  hipError_t FlushCaches() override { return ret(ring_flush_caches(nullptr)); }
+  hipError_t CanAccessPeer(int* can, int dev, int peer) override { return ret(hipDeviceCanAccessPeer(can, dev, peer)); }
   hipError_t P2PAtomics(int* ok, int dev, int peer) override {
     if (dev == peer) {
       *ok = 1;
       return hipSuccess;
     }
-    return hipDeviceGetP2PAttribute(ok, hipDevP2PAttrNativeAtomicSupported, dev, peer);
+    return ret(hipDeviceGetP2PAttribute(ok, hipDevP2PAttrNativeAtomicSupported, dev, peer));
   }
   hipError_t EnablePeerAccess(int peer) override {
     hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
@@ -63,34 +74,41 @@ class HipRuntime final : public DeviceRuntime {
     (void)hipGetLastError();
     return e;
   }
-  hipError_t EventCreate(hipEvent_t* e, unsigned flags) override { return hipEventCreateWithFlags(e, flags); }
-  hipError_t EventDestroy(hipEvent_t e) override { return hipEventDestroy(e); }
-  hipError_t EventRecord(hipEvent_t e, hipStream_t s) override { return hipEventRecord(e, s); }
-  hipError_t EventSynchronize(hipEvent_t e) override { return hipEventSynchronize(e); }
-  hipError_t EventQuery(hipEvent_t e) override { return hipEventQuery(e); }
-  hipError_t StreamCreate(hipStream_t* s) override { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); }
-  hipError_t StreamDestroy(hipStream_t s) override { return hipStreamDestroy(s); }
-  hipError_t StreamSynchronize(hipStream_t s) override { return hipStreamSynchronize(s); }
-  hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) override { return hipStreamWaitEvent(s, e, 0); }
+  hipError_t EventCreate(hipEvent_t* e, unsigned flags) override { return ret(hipEventCreateWithFlags(e, flags)); }
+  hipError_t EventDestroy(hipEvent_t e) override { return ret(hipEventDestroy(e)); }
+  hipError_t EventRecord(hipEvent_t e, hipStream_t s) override { return ret(hipEventRecord(e, s)); }
+  hipError_t EventSynchronize(hipEvent_t e) override { return ret(hipEventSynchronize(e)); }
+  hipError_t EventQuery(hipEvent_t e) override { return ret(hipEventQuery(e)); }
+  hipError_t StreamCreate(hipStream_t* s) override { return ret(hipStreamCreateWithFlags(s, hipStreamNonBlocking)); }
+  hipError_t StreamDestroy(hipStream_t s) override { return ret(hipStreamDestroy(s)); }
+  hipError_t StreamSynchronize(hipStream_t s) override { return ret(hipStreamSynchronize(s)); }
+  hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) override { return ret(hipStreamWaitEvent(s, e, 0)); }
   hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) override {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     hipError_t e = hipStreamIsCapturing(s, &st);
     *capturing = st == hipStreamCaptureStatusActive;
-    return e;
+    return ret(e);
   }
   hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
-    return hipLaunchKernel(fn, grid, block, args, 0, s);
+    return ret(hipLaunchKernel(fn, grid, block, args, 0, s));
   }
   hipError_t LaunchKernelExt(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s,
                              hipEvent_t stop) override {
-    return hipExtLaunchKernel(fn, grid, block, args, 0, s, nullptr, stop, 0);
+    return ret(hipExtLaunchKernel(fn, grid, block, args, 0, s, nullptr, stop, 0));
   }
   hipError_t BlocksPerCu(int* per_cu, const void* fn, int block) override {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, block, 0);
+    return ret(hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, block, 0));
   }
   hipError_t CuCount(int* ncu, int device) override {
-    return hipDeviceGetAttribute(ncu, hipDeviceAttributeMultiprocessorCount, device);
+    return ret(hipDeviceGetAttribute(ncu, hipDeviceAttributeMultiprocessorCount, device));
   }
+  hipError_t IpcGetMemHandle(hipIpcMemHandle_t* h, void* p) override { return ret(hipIpcGetMemHandle(h, p)); }
+  hipError_t IpcOpenMemHandle(void** p, hipIpcMemHandle_t h) override {
+    return ret(hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess));
+  }
+  hipError_t IpcCloseMemHandle(void* p) override { return ret(hipIpcCloseMemHandle(p)); }
+  hipError_t DeviceGetPCIBusId(char* id, int len, int device) override { return ret(hipDeviceGetPCIBusId(id, len, device)); }
+  hipError_t DeviceGetByPCIBusId(int* device, const char* id) override { return ret(hipDeviceGetByPCIBusId(device, id)); }
 };
 
 // Recording fake: "device" memory is host memory tagged with its device,
@@ -100,6 +118,9 @@ class HipRuntime final : public DeviceRuntime {
 //   record dev=D event=E stream=S          stream_wait dev=D stream=S event=E event_dev=D2
 //   host_wait what=event|stream|device|memcpy|error dev=D
 //   peer dev=D peer=P                      flush dev=D
+// Every call is also appended, by name, to a call trace, and any one call can
+// be made to fail: arm(name, nth, err) fails the nth call of that name,
+// counted from arming, with err (tests/test_setup_diag.py walks the setup path this way).
 class FakeRuntime final : public DeviceRuntime {
  public:
   explicit FakeRuntime(int ndev) : ndev_(ndev) {}
@@ -114,7 +135,32 @@ class FakeRuntime final : public DeviceRuntime {
     std::lock_guard<std::mutex> lk(mu_);
     log_.str("");
   }
+  std::string calls(bool clear) {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::string s = calls_.str();
+    if (clear) calls_.str("");
+    return s;
+  }
+  void arm(const char* name, int nth, hipError_t err) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!name) {
+      fail_.clear();
+      return;
+    }
+    fail_[name] = Fail{nth, err, 0};
+  }
+  void delay(const char* name, int ms) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!name) delay_ms_.clear();
+    else delay_ms_[name] = ms;
+  }
+  void live(int* blocks, int* events) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (blocks) *blocks = (int)mem_.size();
+    if (events) *events = (int)events_.size();
+  }
   hipError_t GetDeviceCount(int* n) override {
+    if (hipError_t e = inj("GetDeviceCount")) return e;
     *n = ndev_;
     return hipSuccess;
   }
@@ -127,57 +173,74 @@ class FakeRuntime final : public DeviceRuntime {
     cur_ = d;
     return hipSuccess;
   }
-  hipError_t Malloc(void** p, size_t bytes) override { return alloc(p, bytes, false); }
-  hipError_t MallocUncached(void** p, size_t bytes) override { return alloc(p, bytes, true); }
+  hipError_t Malloc(void** p, size_t bytes) override {
+    if (hipError_t e = inj("Malloc")) return e;
+    return alloc(p, bytes, false);
+  }
+  hipError_t MallocUncached(void** p, size_t bytes) override {
+    if (hipError_t e = inj("MallocUncached")) return e;
+    return alloc(p, bytes, true);
+  }
   bool IsUncached(void* p) override {
     std::lock_guard<std::mutex> lk(mu_);
     auto it = mem_.find(p);
     return it != mem_.end() && it->second.uncached;
   }
   hipError_t Free(void* p) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = mem_.find(p);
-    if (it == mem_.end()) return hipErrorInvalidValue;
-    std::free(p);
-    mem_.erase(it);
-    return hipSuccess;
+    if (hipError_t e = inj("Free")) return e;
+    return release(p);
   }
   hipError_t Memset(void* p, int v, size_t bytes) override {
+    if (hipError_t e = inj("Memset")) return e;
     std::memset(p, v, bytes);
     return hipSuccess;
   }
   hipError_t Memcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind) override {
+    if (hipError_t e = inj("Memcpy")) return e;
     std::memcpy(dst, src, bytes);
     note("host_wait what=memcpy dev=" + std::to_string(cur_));
     return hipSuccess;
   }
-  hipError_t HostMallocMapped(void** p, size_t bytes) override { return alloc(p, bytes, false); }
+  hipError_t HostMallocMapped(void** p, size_t bytes) override {
+    if (hipError_t e = inj("HostMallocMapped")) return e;
+    return alloc(p, bytes, false);
+  }
   hipError_t HostGetDevicePointer(void** d, void* h) override {
+    if (hipError_t e = inj("HostGetDevicePointer")) return e;
     *d = h;
     return hipSuccess;
   }
-  hipError_t HostFree(void* p) override { return Free(p); }
+  hipError_t HostFree(void* p) override {
+    if (hipError_t e = inj("HostFree")) return e;
+    return release(p);
+  }
   hipError_t DeviceSynchronize() override {
+    if (hipError_t e = inj("DeviceSynchronize")) return e;
     note("host_wait what=device dev=" + std::to_string(cur_));
     return hipSuccess;
   }
   hipError_t FlushCaches() override {
+    if (hipError_t e = inj("FlushCaches")) return e;
     note("flush dev=" + std::to_string(cur_));
     return hipSuccess;
   }
   hipError_t CanAccessPeer(int* can, int dev, int peer) override {
+    if (hipError_t e = inj("CanAccessPeer")) return e;
     *can = dev >= 0 && dev < ndev_ && peer >= 0 && peer < ndev_;
     return hipSuccess;
   }
   hipError_t EnablePeerAccess(int peer) override {
+    if (hipError_t e = inj("EnablePeerAccess")) return e;
     note("peer dev=" + std::to_string(cur_) + " peer=" + std::to_string(peer));
     return hipSuccess;
   }
   hipError_t P2PAtomics(int* ok, int dev, int peer) override {
+    if (hipError_t e = inj("P2PAtomics")) return e;
     *ok = dev >= 0 && dev < ndev_ && peer >= 0 && peer < ndev_ && !std::getenv("MCCS_TEST_NO_P2P_ATOMICS");
     return hipSuccess;
   }
   hipError_t EventCreate(hipEvent_t* e, unsigned) override {
+    if (hipError_t r = inj("EventCreate")) return r;
     std::lock_guard<std::mutex> lk(mu_);
     const uintptr_t id = ++next_id_;
     events_[id] = cur_;
@@ -185,37 +248,43 @@ class FakeRuntime final : public DeviceRuntime {
     return hipSuccess;
   }
   hipError_t EventDestroy(hipEvent_t e) override {
+    if (hipError_t r = inj("EventDestroy")) return r;
     std::lock_guard<std::mutex> lk(mu_);
     events_.erase((uintptr_t)e);
     return hipSuccess;
   }
   hipError_t EventRecord(hipEvent_t e, hipStream_t s) override {
+    if (hipError_t r = inj("EventRecord")) return r;
     note("record dev=" + std::to_string(cur_) + " event=" + std::to_string((uintptr_t)e) + " stream=" + sid(s));
     return hipSuccess;
   }
   hipError_t EventSynchronize(hipEvent_t e) override {
+    if (hipError_t r = inj("EventSynchronize")) return r;
     note("host_wait what=event dev=" + std::to_string(event_dev(e)) + " event=" + std::to_string((uintptr_t)e));
     return hipSuccess;
   }
-  hipError_t EventQuery(hipEvent_t) override { return hipSuccess; }
+  hipError_t EventQuery(hipEvent_t) override { return inj("EventQuery"); }
   hipError_t StreamCreate(hipStream_t* s) override {
+    if (hipError_t e = inj("StreamCreate")) return e;
     std::lock_guard<std::mutex> lk(mu_);
     *s = (hipStream_t)(++next_id_);
     return hipSuccess;
   }
-  hipError_t StreamDestroy(hipStream_t) override { return hipSuccess; }
+  hipError_t StreamDestroy(hipStream_t) override { return inj("StreamDestroy"); }
   hipError_t StreamSynchronize(hipStream_t s) override {
+    if (hipError_t e = inj("StreamSynchronize")) return e;
     note("host_wait what=stream dev=" + std::to_string(cur_) + " stream=" + sid(s));
     return hipSuccess;
   }
   hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) override {
+    if (hipError_t r = inj("StreamWaitEvent")) return r;
     note("stream_wait dev=" + std::to_string(cur_) + " stream=" + sid(s) + " event=" +
          std::to_string((uintptr_t)e) + " event_dev=" + std::to_string(event_dev(e)));
     return hipSuccess;
   }
   hipError_t StreamIsCapturing(hipStream_t, bool* capturing) override {
     *capturing = false;
-    return hipSuccess;
+    return inj("StreamIsCapturing");
   }
   hipError_t LaunchKernelExt(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s,
                              hipEvent_t stop) override {
@@ -225,6 +294,7 @@ class FakeRuntime final : public DeviceRuntime {
     return e;
   }
   hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
+    if (hipError_t e = inj("LaunchKernel")) return e;
     // every communicator of a fused ring launch must live on the launching device
     bool on_dev = true;
     unsigned inl = 0;
@@ -262,10 +332,53 @@ class FakeRuntime final : public DeviceRuntime {
   }
   hipError_t BlocksPerCu(int* per_cu, const void*, int) override {
     *per_cu = 1;
-    return hipSuccess;
+    return inj("BlocksPerCu");
   }
   hipError_t CuCount(int* ncu, int) override {
     *ncu = 256;
+    return inj("CuCount");
+  }
+  // IPC within one process: the handle carries the block's address (every
+  // fake "process" is this one), opening checks that the block is alive
+  hipError_t IpcGetMemHandle(hipIpcMemHandle_t* h, void* p) override {
+    if (hipError_t e = inj("IpcGetMemHandle")) return e;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!mem_.count(p)) return hipErrorInvalidValue;
+    std::memset(h, 0, sizeof(*h));
+    std::memcpy(h->reserved, "FAKEIPC", 8);
+    std::memcpy(h->reserved + 8, &p, sizeof(p));
+    return hipSuccess;
+  }
+  hipError_t IpcOpenMemHandle(void** p, hipIpcMemHandle_t h) override {
+    if (hipError_t e = inj("IpcOpenMemHandle")) return e;
+    void* q = nullptr;
+    std::memcpy(&q, h.reserved + 8, sizeof(q));
+    std::lock_guard<std::mutex> lk(mu_);
+    if (std::memcmp(h.reserved, "FAKEIPC", 8) != 0 || !mem_.count(q)) return hipErrorInvalidValue;
+    ++ipc_open_[q];
+    *p = q;
+    return hipSuccess;
+  }
+  hipError_t IpcCloseMemHandle(void* p) override {
+    if (hipError_t e = inj("IpcCloseMemHandle")) return e;
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = ipc_open_.find(p);
+    if (it == ipc_open_.end()) return hipErrorInvalidValue;
+    if (--it->second == 0) ipc_open_.erase(it);
+    return hipSuccess;
+  }
+  hipError_t DeviceGetPCIBusId(char* id, int len, int device) override {
+    if (hipError_t e = inj("DeviceGetPCIBusId")) return e;
+    if (device < 0 || device >= ndev_) return hipErrorInvalidDevice;
+    std::snprintf(id, (size_t)len, "0000:%02x:00.0", 0x10 + device);
+    return hipSuccess;
+  }
+  hipError_t DeviceGetByPCIBusId(int* device, const char* id) override {
+    if (hipError_t e = inj("DeviceGetByPCIBusId")) return e;
+    unsigned bus = 0;
+    if (std::sscanf(id, "0000:%x:00.0", &bus) != 1 || bus < 0x10 || (int)bus - 0x10 >= ndev_)
+      return hipErrorInvalidValue;
+    *device = (int)bus - 0x10;
     return hipSuccess;
   }
 
@@ -274,12 +387,46 @@ class FakeRuntime final : public DeviceRuntime {
     int device;
     bool uncached;
   };
+  struct Fail {
+    int nth;  // 1-based among this name's calls since arming; 0 = every call
+    hipError_t err;
+    int seen;
+  };
+  // Traces the call, sleeps for its armed delay (outside the lock: other
+  // threads' calls go on meanwhile), and returns the armed error for it, if
+  // this is the one.
+  hipError_t inj(const char* name) {
+    int delay = 0;
+    hipError_t e = hipSuccess;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      calls_ << name << '\n';
+      auto d = delay_ms_.find(name);
+      if (d != delay_ms_.end()) delay = d->second;
+      auto it = fail_.find(name);
+      if (it != fail_.end()) {
+        Fail& f = it->second;
+        ++f.seen;
+        if (f.nth == 0 || f.seen == f.nth) e = f.err;
+      }
+    }
+    if (delay > 0) std::this_thread::sleep_for(std::chrono::milliseconds(delay));
+    return e;
+  }
   hipError_t alloc(void** p, size_t bytes, bool uncached) {
     void* q = std::calloc(1, bytes ? bytes : 1);
     if (!q) return hipErrorOutOfMemory;
     std::lock_guard<std::mutex> lk(mu_);
     mem_[q] = Block{cur_, uncached};
     *p = q;
+    return hipSuccess;
+  }
+  hipError_t release(void* p) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = mem_.find(p);
+    if (it == mem_.end()) return hipErrorInvalidValue;
+    std::free(p);
+    mem_.erase(it);
     return hipSuccess;
   }
   int dev_of(const void* p) {
@@ -303,7 +450,10 @@ class FakeRuntime final : public DeviceRuntime {
   std::mutex mu_;
   std::map<void*, Block> mem_;
   std::map<uintptr_t, int> events_;
-  std::ostringstream log_;
+  std::map<void*, int> ipc_open_;
+  std::map<std::string, Fail> fail_;
+  std::map<std::string, int> delay_ms_;
+  std::ostringstream log_, calls_;
 };
 
 HipRuntime g_hip;
@@ -367,4 +517,51 @@ extern "C" int mccs_test_fake_log(char* buf, int cap, int clear) {
   }
   if (clear) f->clear();
   return (int)s.size();
+}
+
+// Fails the nth call (1-based, counted from now; 0 = every call) of the fake
+// runtime's method `call` (its DeviceRuntime name, e.g. "HostMallocMapped")
+// with hipError_t `err`; call = NULL disarms every injection.  -1 without a fake.
+extern "C" int mccs_test_fake_fail(const char* call, int nth, int err) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  f->arm(call, nth, (hipError_t)err);
+  return 0;
+}
+
+// The fake's call trace (method names, one a line) since the last clear; same
+// contract as mccs_test_fake_log.
+extern "C" int mccs_test_fake_calls(char* buf, int cap, int clear) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  const std::string s = f->calls(clear != 0);
+  if (buf && cap > 0) {
+    const size_t n = std::min(s.size(), (size_t)cap - 1);
+    std::memcpy(buf, s.data(), n);
+    buf[n] = '\0';
+  }
+  return (int)s.size();
+}
+
+// Live fake allocations (device + host blocks) and events, and the FIFO
+// arenas the process pool holds (pooled arenas stay allocated by design).
+extern "C" int mccs_test_fake_live(int* blocks, int* events, int* pooled) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  f->live(blocks, events);
+  if (pooled) *pooled = mccs::comm_pool_count(mccs::rt_generation());
+  return 0;
+}
+
+// Makes every call of the fake's method `call` sleep `ms` milliseconds before
+// returning (lock-holding tests: ADVICE r04); call = NULL clears all delays.
+extern "C" int mccs_test_fake_delay(const char* call, int ms) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  f->delay(call, ms);
+  return 0;
 }

@@ -5,8 +5,10 @@
 // rt(): the HIP runtime in production, or a recording fake with N pretend
 // devices (host memory, no kernels run) that CPU tests install with
 // mccs_test_fake_runtime() to check how launches are issued across devices
-// (tests/test_multidevice_launch.py).  The IPC (one rank per process) and
-// shared-memory service paths call HIP directly: they need a real GPU.
+// (tests/test_multidevice_launch.py).  Per-rank setup and connect (one rank
+// per process) go through it too, so the fake can fail any one of their calls
+// (mccs_test_fake_fail, tests/test_setup_diag.py).  The shared-memory service
+// path calls HIP directly: it needs a real GPU.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -52,6 +54,12 @@ class DeviceRuntime {
                                      hipEvent_t stop) = 0;
   virtual hipError_t BlocksPerCu(int* per_cu, const void* fn, int block) = 0;
   virtual hipError_t CuCount(int* ncu, int device) = 0;
+  // one rank per process (mccsCommSetupRank / mccsCommConnect)
+  virtual hipError_t IpcGetMemHandle(hipIpcMemHandle_t* h, void* p) = 0;
+  virtual hipError_t IpcOpenMemHandle(void** p, hipIpcMemHandle_t h) = 0;  // lazy peer access
+  virtual hipError_t IpcCloseMemHandle(void* p) = 0;
+  virtual hipError_t DeviceGetPCIBusId(char* id, int len, int device) = 0;
+  virtual hipError_t DeviceGetByPCIBusId(int* device, const char* id) = 0;
 };
 
 DeviceRuntime& rt();

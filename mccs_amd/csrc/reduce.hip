@@ -270,6 +270,15 @@ static int num_cus() {
   return n;
 }
 
+// A launch's own status.  hipGetLastError() after a launch would also return
+// any earlier failure left on the calling thread by another call (the
+// caller's, another library's), reporting it as this launch's.
+template <typename K>
+static hipError_t launch_k(K k, int grid, int block, size_t lds, hipStream_t st, const ReduceArgs& a) {
+  void* args[] = {(void*)&a};
+  return hipLaunchKernel((const void*)k, dim3(grid), dim3(block), args, lds, st);
+}
+
 template <int DT, int OP>
 constexpr bool tuned_grid() { return OP == OpSum && (DT == mccsFloat32 || DT == mccsFloat16 || DT == mccsBfloat16); }
 
@@ -277,22 +286,14 @@ constexpr bool tuned_grid() { return OP == OpSum && (DT == mccsFloat32 || DT == 
 // 3 plain loads + nt stores (2/3 and map 1 only in the tuning grid).
 template <int DT, int OP, int NS, int ND, int U, int MAP>
 static hipError_t launch_reg(const ReduceArgs& a, int pol, int grid, hipStream_t st) {
-#define MCCS_REG(LP, SP) \
-  hipLaunchKernelGGL((reduce_reg_kernel<DT, OP, NS, ND, U, LP, SP, MAP>), dim3(grid), dim3(256), 0, st, a)
+#define MCCS_REG(LP, SP) launch_k((reduce_reg_kernel<DT, OP, NS, ND, U, LP, SP, MAP>), grid, 256, 0, st, a)
   if constexpr (tuned_grid<DT, OP>()) {
-    if (pol == 2) {
-      MCCS_REG(kNonTemporal, kPlain);
-      return hipGetLastError();
-    }
-    if (pol == 3) {
-      MCCS_REG(kPlain, kNonTemporal);
-      return hipGetLastError();
-    }
+    if (pol == 2) return MCCS_REG(kNonTemporal, kPlain);
+    if (pol == 3) return MCCS_REG(kPlain, kNonTemporal);
   }
-  if (pol) MCCS_REG(kNonTemporal, kNonTemporal);
-  else MCCS_REG(kPlain, kPlain);
+  if (pol) return MCCS_REG(kNonTemporal, kNonTemporal);
+  return MCCS_REG(kPlain, kPlain);
 #undef MCCS_REG
-  return hipGetLastError();
 }
 
 template <int DT, int OP, int NS, int ND>
@@ -353,8 +354,7 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
       int64_t blocks = (wtiles + W - 1) / W;
       const int64_t gmax = g_grid_cap > 0 ? g_grid_cap : (int64_t)num_cus() * bpc;
       const int grid = (int)(blocks < gmax ? (blocks > 0 ? blocks : 1) : gmax);
-      hipLaunchKernelGGL(kw, dim3(grid), dim3(W * 64), lds, st, a);
-      return hipGetLastError();
+      return launch_k(kw, grid, W * 64, lds, st, a);
     }
   }
   constexpr int PACK = kPackElems<DT>;
@@ -363,13 +363,9 @@ static hipError_t launch_lds(const ReduceArgs& a, int pol, int bpc, hipStream_t 
   int64_t blocks = (wtiles + W - 1) / W;
   const int64_t gmax = g_grid_cap > 0 ? g_grid_cap : (int64_t)num_cus() * bpc;
   const int grid = (int)(blocks < gmax ? (blocks > 0 ? blocks : 1) : gmax);
-  if (pol == 1 || pol >= 3)
-    hipLaunchKernelGGL(kn, dim3(grid), dim3(W * 64), lds, st, a);
-  else if (pol == 2)
-    hipLaunchKernelGGL(ks, dim3(grid), dim3(W * 64), lds, st, a);
-  else
-    hipLaunchKernelGGL(kp, dim3(grid), dim3(W * 64), lds, st, a);
-  return hipGetLastError();
+  if (pol == 1 || pol >= 3) return launch_k(kn, grid, W * 64, lds, st, a);
+  if (pol == 2) return launch_k(ks, grid, W * 64, lds, st, a);
+  return launch_k(kp, grid, W * 64, lds, st, a);
 }
 
 // (U, S, W) run-time -> template.  The default (2, 3, 4) exists for every
@@ -401,8 +397,7 @@ static hipError_t dispatch(const ReduceArgs& a, hipStream_t st) {
   if (mis & 15) {
     int64_t blocks = (a.count + 255) / 256;
     int grid = (int)(blocks < (int64_t)cus * 8 ? (blocks > 0 ? blocks : 1) : (int64_t)cus * 8);
-    hipLaunchKernelGGL((reduce_scalar_kernel<DT, OP>), dim3(grid), dim3(256), 0, st, a);
-    return hipGetLastError();
+    return launch_k((reduce_scalar_kernel<DT, OP>), grid, 256, 0, st, a);
   }
   if (t.variant == MCCS_REDUCE_VARIANT_LDS && a.nsrcs == 2 && a.ndsts == 1) {
     bool ok = false;

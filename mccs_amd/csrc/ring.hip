@@ -67,9 +67,12 @@ __global__ void cache_flush_kernel() {
   }
 }
 
+// Returns the launch's own status.  It used to return hipGetLastError(),
+// which also reports any failure an earlier call left on the calling thread
+// (the caller's, torch's, a handled one of ours): communicator setup then
+// failed on an error that was not its own (tests/test_setup_diag.py).
 hipError_t ring_flush_caches(hipStream_t st) {
-  hipLaunchKernelGGL(cache_flush_kernel, dim3(2048), dim3(64), 0, st);
-  return hipGetLastError();
+  return hipLaunchKernel((const void*)cache_flush_kernel, dim3(2048), dim3(64), nullptr, 0, st);
 }
 
 // Reads (and optionally zeroes) the current device's ring profile counters,
@@ -118,6 +121,7 @@ bool colocated_launch_running(int device, const mccsDevComm* comm) {
         ++i;
         continue;
       }
+      if (q != hipSuccess) (void)hipGetLastError();  // a failed launch's event: forget it, leave no stale error
       (void)hipEventDestroy(x.done);
       g_ext.erase(g_ext.begin() + i);
       continue;

@@ -20,13 +20,18 @@ fresh communicator:
              variant (they share one control block), not a dead communicator;
              both ranks keep the ring, exact;
   mismatch   ranks resolve different one-shot thresholds that round to the
-             same arena: Connect refuses on every rank.
+             same arena (ADVICE r03): Connect refuses on every rank;
+  late       rank 1 enters Connect 8 s after rank 0 (the gate's
+             first launch used to time out after 5 s on the early rank); the
+             connect-time barrier waits under the configured 20 s watchdog,
+             and the gate then passes as in "clean".
 After each connect, exact-sum AllReduces at LL / one-shot / ring sizes check
 the results and which kernel ran.
 """
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -56,7 +61,14 @@ def main():
     cases = {"clean": {}, "ring": {"MCCS_GATE_INJECT": hex(G_RING_UC), "MCCS_GATE_INJECT_RANK": "1"},
              "oneshot": {"MCCS_GATE_INJECT": hex(G_ONE), "MCCS_GATE_INJECT_RANK": "0"},
              "hang": {"MCCS_GATE_SKIP": hex(G_LL), "MCCS_GATE_INJECT_RANK": "1"},
-             "mismatch": {"MCCS_ONESHOT_BYTES": "1000000" if rank == 0 else "1048576"}}
+             "mismatch": {"MCCS_ONESHOT_BYTES": "1000000" if rank == 0 else "1048576"},
+             "late": {}}
+
+    def late_exchange(b):
+        out = exchange(b)
+        if rank == 1:
+            time.sleep(8.0)
+        return out
     results = {}
     dv = torch.device("cuda", dev)
     for name, env in cases.items():
@@ -66,7 +78,8 @@ def main():
         os.environ.update(env)
         dist.barrier()
         try:
-            comm = C.init_communicator_rank(rank, world, dev, exchange, C.CommConfig(timeout_ms=20000))
+            comm = C.init_communicator_rank(rank, world, dev, late_exchange if name == "late" else exchange,
+                                            C.CommConfig(timeout_ms=20000))
         except RuntimeError as e:
             results[f"{name}/connect"] = {"ok": name == "mismatch" and "mccsCommConnect" in str(e), "err": str(e)[:200]}
             continue

@@ -7,7 +7,8 @@ ring vote; a wrong one-shot sum injected on the other rank disables the
 one-shot on both; a direct launch left hanging (the peer never launches it)
 ends at the 5 s watchdog as a vote against every direct variant while the
 ring stays usable; thresholds that differ but round to the same arena make
-Connect refuse on both.  Every AllReduce after a gate is
+Connect refuse on both; a rank that enters Connect 8 s late is
+waited for by the connect-time barrier.  Every AllReduce after a gate is
 checked exact and for the kernel it took.
 """
 import json
@@ -38,4 +39,5 @@ def test_gate_verdicts_agree_across_processes():
     assert r.returncode == 0 and lines, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(lines[-1])
     assert res["all_ok"], res
-    assert set(res["cases"]) >= {"clean/gate", "ring/gate", "oneshot/gate", "hang/gate", "mismatch/connect"}
+    assert set(res["cases"]) >= {"clean/gate", "ring/gate", "oneshot/gate", "hang/gate", "mismatch/connect",
+                                 "late/gate"}
