@@ -139,6 +139,11 @@ SIGNATURES: dict[str, tuple] = {
                  _P(_c_int)]),
 }
 
+# Symbols appended after round 4: an older build (an A/B library under abvar/,
+# MCCS_LIB_PATH) loads without them; the in-tree build must export them
+# (tests/test_lib_exports.py).
+_ADDED_R5 = {"mccsGetLastErrorString", "mccsGetLastHipError"}
+
 _lib = None
 
 
@@ -154,6 +159,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
         )
     lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
+        if name in _ADDED_R5 and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -166,7 +173,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
 
 def last_error() -> str:
     """The calling thread's diagnosis of its latest failed library call ("" if none)."""
-    return _lib.mccsGetLastErrorString().decode(errors="replace") if _lib is not None else ""
+    if _lib is None or not hasattr(_lib, "mccsGetLastErrorString"):
+        return ""
+    return _lib.mccsGetLastErrorString().decode(errors="replace")
 
 
 def check(code: int, what: str) -> None:

@@ -33,28 +33,6 @@ __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
   else *p = v;
 }
 
-// The first pass of source 0 of reduce_copy_rows, loaded ahead (the ring's
-// user input does not depend on the peer's flag, so a data wave issues these
-// loads before it waits for the slice to become ready).  Returns false (and
-// loads nothing) when reduce_copy_rows will take its unaligned path.
-template <int DT, int U, int NTMASK, int PF>
-__device__ __forceinline__ bool prefetch_rows_a(const void* s0, const void* s1, const void* d0, const void* d1,
-                                                int64_t nelem, int tid, int nthr, u32x4 (&v)[PF]) {
-  constexpr int PACK = kPackElems<DT>;
-  if (nelem <= 0 || (((uintptr_t)s0 | (uintptr_t)s1 | (uintptr_t)d0 | (uintptr_t)d1) & 15)) return false;
-  const uint32_t npack = (uint32_t)(nelem / PACK);
-  // shorter than one pass: reduce_copy_rows runs only its predicated pass
-  if (npack >= ((uint32_t)nthr >> 6) * 64u * U) return false;
-  const uint32_t wave = (uint32_t)tid >> 6, lane = (uint32_t)tid & 63;
-  if (wave >= ((uint32_t)nthr >> 6)) return true;  // a partial last wave has no rows
-  const uint32_t mine = wave * (64u * U) + lane;
-  const u32x4* a = (const u32x4*)s0;
-#pragma unroll
-  for (int u = 0; u < PF; ++u)
-    if (mine + 64u * u < npack) v[u] = ld16<(NTMASK & 1) ? kNonTemporal : kPlain>(a + mine + 64u * u);
-  return true;
-}
-
 // Ring-step reduce-copy with the operand shape fixed at compile time (the
 // ring primitive knows it: NS sources, ND destinations) and a wave-contiguous
 // layout: wave w of the group owns U consecutive 1 KiB rows of each U*W KiB
@@ -65,12 +43,10 @@ __device__ __forceinline__ bool prefetch_rows_a(const void* s0, const void* s1, 
 // iteration are issued before the first use; the partial last iteration is a
 // single predicated pass.  Every pointer must be 16-byte aligned when
 // ALIGNED; otherwise a typed element loop runs (reference ReduceCopyMulti).
-// DP0 / DP1: store policy of destination 0 / 1.  use_pre: pre holds the
-// first PF packs of source 0, already loaded by prefetch_rows_a (only for a
-// slice shorter than one pass, which takes the predicated pass alone).
-template <int DT, int OP, int U, int NS, int ND, int NTMASK, int DP0 = kPlain, int DP1 = kPlain, int PF = 1>
+// DP0 / DP1: store policy of destination 0 / 1.
+template <int DT, int OP, int U, int NS, int ND, int NTMASK, int DP0 = kPlain, int DP1 = kPlain>
 __device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1, void* d0, void* d1, int64_t nelem,
-                                                 int tid, int nthr, bool use_pre, const u32x4 (&pre)[PF]) {
+                                                 int tid, int nthr) {
   static_assert(NS >= 1 && NS <= 2 && ND >= 1 && ND <= 2, "ring primitives move 1-2 sources to 1-2 destinations");
   using T = typename Elem<DT>::T;
   constexpr int PACK = kPackElems<DT>;
@@ -116,9 +92,7 @@ __device__ __forceinline__ void reduce_copy_rows(const void* s0, const void* s1,
       u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (q + 64u * u < npack)
-          v[u] = (u < PF && use_pre && base == 0) ? pre[u < PF ? u : 0]
-                                                  : ld16<(NTMASK & 1) ? kNonTemporal : kPlain>(a + q + 64u * u);
+        if (q + 64u * u < npack) v[u] = ld16<(NTMASK & 1) ? kNonTemporal : kPlain>(a + q + 64u * u);
       if constexpr (NS > 1) {
         u32x4 w[U];
 #pragma unroll

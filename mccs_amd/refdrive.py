@@ -575,18 +575,28 @@ def default_variants(world: int, default_rings, max_channels: int = 32) -> list[
     ]
 
 
+# Send/recv pairs the timed loop rotates through, per rank: at least this
+# many bytes, as bench.py's N = 1 loop rotates (bench.py --rotate-mib), so
+# no call finds its input in the 256 MB last-level cache from the call
+# before (a same-buffer loop flatters plain input loads).
+ROTATE_BYTES = 1152 << 20
+
+
 def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbytes: int, variants: list[dict],
-                          warmup: int = 3, steps: int = 10, group=None) -> list[dict]:
+                          warmup: int = 3, steps: int = 10, group=None, rotate_bytes: int = ROTATE_BYTES) -> list[dict]:
     """Times every variant at `nbytes` fp32 per rank (algbw = nbytes / t per
     AllReduce, max over ranks), each gated by an exact-sum check on every
-    rank.  Ranks must be one per process; `dist` carries the handle exchange
-    and barriers (gloo)."""
+    rank.  Step i uses send/recv pair i mod P, P = ceil(rotate_bytes /
+    2 nbytes) (1 = one pair reused: the same-buffer figure).  Ranks must be
+    one per process; `dist` carries the handle exchange and barriers (gloo)."""
     dtype, code = torch.float32, 7
     count = nbytes // 4
     dev = torch.device("cuda", device)
-    send = exact_inputs(torch, count, rank, dtype, dev)
+    npairs = max(1, -(-rotate_bytes // (2 * nbytes))) if rotate_bytes > 0 else 1
+    sends = [exact_inputs(torch, count, rank, dtype, dev) for _ in range(npairs)]
+    recvs = [torch.empty_like(sends[0]) for _ in range(npairs)]
+    send, recv = sends[0], recvs[0]
     want = expected_exact(torch, count, world, dtype, dev)
-    recv = torch.empty_like(send)
     from ._streams import side_stream
 
     stream = side_stream(torch, device, slot=1)
@@ -613,7 +623,7 @@ def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbyte
     out = []
     for v in variants:
         res = {"variant": v["name"], "channels": v["nch"], "locality": v["locality"],
-               "fifo": v.get("fifo", "device")}
+               "fifo": v.get("fifo", "device"), "buffer_pairs_rotated": npairs}
         rr, err = None, None
         try:
             rr = RefDrivenRank(rank, world, device, allgather, nch=v["nch"], rings=v["rings"],
@@ -637,19 +647,27 @@ def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbyte
             if ok:
                 el = float("inf")
                 try:
-                    for _ in range(warmup):
-                        rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+                    for i in range(warmup):
+                        rr.all_reduce(sends[i % npairs].data_ptr(), recvs[i % npairs].data_ptr(), count, code, 0,
+                                      stream.cuda_stream)
                     stream.synchronize()
                 except Exception as e:  # noqa: BLE001
                     err = f"warmup: {type(e).__name__}: {e}"[:300]
                 barrier()
                 try:
+                    for r_ in recvs:
+                        r_.zero_()
+                    torch.cuda.synchronize(dev)
+                    barrier()
                     t0 = time.perf_counter()
-                    for _ in range(steps):
-                        rr.all_reduce(send.data_ptr(), recv.data_ptr(), count, code, 0, stream.cuda_stream)
+                    for i in range(steps):
+                        rr.all_reduce(sends[i % npairs].data_ptr(), recvs[i % npairs].data_ptr(), count, code, 0,
+                                      stream.cuda_stream)
                     stream.synchronize()
                     el = time.perf_counter() - t0
-                    ok2 = bool(torch.equal(recv, want)) and not rr.aborted()
+                    # every pair the timed loop wrote holds the exact sum
+                    ok2 = all(bool(torch.equal(recvs[i], want)) for i in range(min(steps, npairs))) and \
+                        not rr.aborted()
                 except Exception as e:  # noqa: BLE001
                     err, ok2 = f"timing: {type(e).__name__}: {e}"[:300], False
                 el = max_over_ranks(el)

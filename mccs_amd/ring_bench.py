@@ -41,6 +41,69 @@ class BenchFailure(SystemExit):
     """A correctness gate failed on some rank: the bench exits non-zero."""
 
 
+# Wall-clock budget of one N > 1 run (MCCS_BENCH_BUDGET_S overrides).  The
+# 1-GPU rehearsals of the whole line took 27-60 s at N = 8; on a node the
+# autotune connects up to 12 candidates (each with its node gate) and every
+# extra leg moves more bytes, so the default leaves room for that while
+# staying well inside a driver limit of 10+ minutes for the whole command
+# (torchrun start, imports, first-touch of 8 GPUs included).
+DEFAULT_BUDGET_S = 360.0
+AUTOTUNE_SHARE = 0.35  # of the budget: later candidates are skipped past it
+# Expected wall time of each extra leg on a node (s): a leg starts only if
+# this much budget is left.  From the 1-GPU rehearsals' per-leg wall_s with
+# margin for a node's slower first touches.
+LEG_NEED_S = {"graph_replay": 5, "configs3_fp16_1GiB": 20, "allgather_16MiB_per_rank": 8, "size_sweep_fp16": 25,
+              "direct_sweep_fp16": 40, "configs4_two_jobs": 45, "reference_driven": 60, "node_legs": 40,
+              "cpu_ring_baseline": 8}
+
+
+class Budget:
+    """Wall-clock budget of one N > 1 bench run (the line ran
+    about 12 legs before printing anything, bounded only by per-kernel
+    watchdogs).  The headline -- the autotune's candidates up to its share,
+    the timed steps and their exact-sum gates, the CPU baseline -- always
+    runs.  Every other leg runs only if, when it would start, the budget left
+    covers its expected time; the decision is agreed over all ranks (the legs
+    are collective, so every rank must take the same branch).  `legs` records
+    each leg's wall time or its skip, and goes into the line."""
+
+    def __init__(self, dist, seconds=None, clock=time.monotonic, group=None):
+        if seconds is None:
+            seconds = float(os.environ.get("MCCS_BENCH_BUDGET_S", DEFAULT_BUDGET_S))
+        self.dist, self.seconds, self.clock, self.group = dist, float(seconds), clock, group
+        self.t0 = clock()
+        self.legs: dict = {}
+
+    def elapsed(self) -> float:
+        return self.clock() - self.t0
+
+    def allow(self, name: str, need_s: float | None = None) -> bool:
+        need = LEG_NEED_S.get(name, 0.0) if need_s is None else need_s
+        at = self.elapsed()
+        if agree(self.dist, at + need <= self.seconds, self.group):
+            return True
+        self.legs[name] = {"skipped": "budget", "at_s": round(at, 2), "need_s": need}
+        return False
+
+    def run(self, name: str, fn, need_s: float | None = None):
+        """fn() if the budget allows it (its wall time recorded), else None."""
+        if not self.allow(name, need_s):
+            return None
+        t = self.clock()
+        out = fn()
+        self.legs[name] = {"wall_s": round(self.clock() - t, 2)}
+        return out
+
+    def note(self, name: str, t_start: float) -> None:
+        """Records a leg that always runs (started at clock value t_start)."""
+        self.legs[name] = {"wall_s": round(self.clock() - t_start, 2)}
+
+    def summary(self) -> dict:
+        return {"budget_s": self.seconds, "elapsed_s": round(self.elapsed(), 2), "legs": self.legs,
+                "note": "a leg starts only if the budget left covers its expected time (LEG_NEED_S); "
+                        "the headline timing and its gates always run"}
+
+
 def _exchange_factory(dist, world, group=None):
     """Connect-handle all-gather over the control plane (replaces the
     reference's bootstrap ring + exchange engine for this path)."""
@@ -207,7 +270,7 @@ def make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, mode
 
 
 def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for, warmup=2, reps=6,
-             ranks_share_gpu=False, rejected=None):
+             ranks_share_gpu=False, rejected=None, budget=None):
     """Transport placement chosen on the node itself: FIFO data at the
     receiver (remote writes) or at the sender (remote reads, the reference's
     SHM layout), each at the auto lane count and at 16 and 32 lanes per
@@ -216,6 +279,8 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
     most MAX_RING_WORKGROUPS workgroups per rank).
     Every candidate passes the exact-sum gate; the fastest (max over ranks)
     is kept.  MCCS_LOCALITY / MCCS_LANES / MCCS_CHANNELS pin a dimension.
+    With a `budget`, candidates after the first one that passed are tried
+    only while the autotune has used less than AUTOTUNE_SHARE of it.
     Returns (comm, mode, table)."""
     locs = [None] if "MCCS_LOCALITY" in os.environ else [C.LOCALITY_RECEIVER, C.LOCALITY_SENDER]
     # lanes per channel: auto (64 / channels; 9 at n = 8), 16 and 32 -- more
@@ -226,6 +291,10 @@ def autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
     chan_opts = channel_options(C, world, ranks_share_gpu)
     best, table, seen = None, [], set()
     for label, modes in _candidates(C, lanes_opts, locs, chan_opts):
+        if best is not None and budget is not None and not budget.allow(
+                f"autotune:{label}", budget.seconds * (1 - AUTOTUNE_SHARE)):
+            table.append({"mode": label, "skipped": "budget"})
+            continue
         comm, mode = make_validated_comm(torch, dist, C, rank, world, device, dev, exchange, modes, full,
                                          rejected=rejected)
         if comm is None:
@@ -685,6 +754,7 @@ def run(args, cpu_sum_baseline=None):
 
 
 def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_baseline=None):
+    budget = Budget(dist)
     exchange = _exchange_factory(dist, world)
     dt_name = args.dtype
     tdt = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[dt_name]
@@ -708,6 +778,7 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
     tune_table = None
     share = ndev < world
     rejected = []
+    t = budget.clock()
     if getattr(args, "no_autotune", False):
         lanes = shared_gpu_lanes(world) if share and "MCCS_LANES" not in os.environ else None
         comm, mode = make_validated_comm(torch, dist, C, rank, world, device, dev, exchange,
@@ -716,7 +787,9 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
             raise BenchFailure("no FIFO mode passed the exact-sum gate before timing")
     else:
         comm, mode, tune_table = autotune(torch, dist, C, rank, world, device, dev, exchange, full, step_for,
-                                          ranks_share_gpu=share, rejected=rejected)
+                                          ranks_share_gpu=share, rejected=rejected, budget=budget)
+    budget.note("autotune", t)
+    t = budget.clock()
     K = args.steps
     C.ring_profile(device, reset=True)
     per_step = max_over_ranks(dist, time_steps(torch, dist, comm, step_for(comm), args.warmup, K)) / K
@@ -725,19 +798,30 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
     if os.environ.get("MCCS_BENCH_INJECT_MISMATCH") == "1":
         ok = False  # fault injection: the bench must exit non-zero
     require(dist, ok, "full-size exact-sum AllReduce after timing")
+    budget.note("headline", t)
     extras = {"rejected_before_timing": [{k: v for k, v in r.items() if v is not None} for r in rejected]}
-    if not getattr(args, "no_extra", False):
-        gr = graph_replay(torch, dist, comm, lambda st: C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, st))
-        extras["graph_replay"] = {
-            "ms_per_step": round(gr * 1e3, 4), "algbw_GBps": round(nbytes / gr / 1e9, 3),
-            "note": "the same AllReduce captured 10x in one HIP graph and replayed (no host path per call); "
-                    "value above is the eager path"}
+    # connect (+ node gate) time of the timed communicator on every rank
+    timings = [None] * world
+    dist.all_gather_object(timings, getattr(comm, "connect_timing", None))
+    extras["connect_timing_per_rank"] = timings
+    extra = not getattr(args, "no_extra", False)
+    if extra:
+        def _graph():
+            gr = graph_replay(torch, dist, comm,
+                              lambda st: C.all_reduce(comm, x, y, n, code, C.AllReduceOpType.Sum, st))
+            return {"ms_per_step": round(gr * 1e3, 4), "algbw_GBps": round(nbytes / gr / 1e9, 3),
+                    "note": "the same AllReduce captured 10x in one HIP graph and replayed (no host path per "
+                            "call); value above is the eager path"}
+        extras["graph_replay"] = budget.run("graph_replay", _graph)
     del x, y
     torch.cuda.empty_cache()
-    if not getattr(args, "no_extra", False) and (dt_name, args.size_mib) == ("float32", 128):
-        extras["configs3_fp16_1GiB"] = extra_fp16_1gib(torch, dist, C, comm, rank, world, dev)
-        extras["allgather_16MiB_per_rank"] = extra_allgather(torch, dist, C, comm, rank, world, dev)
-        extras["size_sweep_fp16"] = size_sweep(torch, dist, C, comm, rank, world, dev)
+    if extra and (dt_name, args.size_mib) == ("float32", 128):
+        extras["configs3_fp16_1GiB"] = budget.run(
+            "configs3_fp16_1GiB", lambda: extra_fp16_1gib(torch, dist, C, comm, rank, world, dev))
+        extras["allgather_16MiB_per_rank"] = budget.run(
+            "allgather_16MiB_per_rank", lambda: extra_allgather(torch, dist, C, comm, rank, world, dev))
+        extras["size_sweep_fp16"] = budget.run(
+            "size_sweep_fp16", lambda: size_sweep(torch, dist, C, comm, rank, world, dev))
     info = {"channels": comm.nchannels, "lanes": comm.lanes, "block_threads": comm.block_threads}
     # the connect-time node gate of the timed communicator (csrc/host/gate.cpp):
     # whether it ran, the hand-off it left (MCCS_FIFO_* code: what the line
@@ -748,38 +832,50 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
                            "bits": "0x1 ring uncached, 0x2 ring release, 0x4 ring system, 0x8 LL, 0x10 one-shot, "
                                    "0x20 two-shot, 0x40 no peer atomics",
                            "fifo_memory_codes": "0 uncached (relaxed), 1 cached + system fences, 2 uncached + release"}
-    if not getattr(args, "no_extra", False) and "size_sweep_fp16" in extras and 2 <= world <= 8:
-        extras["direct_sweep_fp16"] = direct_sweep(torch, dist, C, rank, world, device, dev, exchange,
-                                                   mode_config(C, mode, info), extras["size_sweep_fp16"])
+    if extra and extras.get("size_sweep_fp16") and 2 <= world <= 8:
+        extras["direct_sweep_fp16"] = budget.run(
+            "direct_sweep_fp16", lambda: direct_sweep(torch, dist, C, rank, world, device, dev, exchange,
+                                                      mode_config(C, mode, info), extras["size_sweep_fp16"]))
     rings = comm.rings()
     comm.destroy()
-    if (not getattr(args, "no_extra", False) and world % 2 == 0
-            and world >= int(os.environ.get("MCCS_BENCH_SETUP2_MIN_WORLD", "8"))):
+    if extra and world % 2 == 0 and world >= int(os.environ.get("MCCS_BENCH_SETUP2_MIN_WORLD", "8")):
         # BASELINE configs[4] on a full node: the two trace jobs on disjoint halves
-        extras["configs4_two_jobs"] = setup2_measure(torch, dist, C, rank, world, device, dev, False,
-                                                     warmup=1, iters=int(os.environ.get("MCCS_SETUP2_ITERS", "10")))
+        extras["configs4_two_jobs"] = budget.run(
+            "configs4_two_jobs", lambda: setup2_measure(torch, dist, C, rank, world, device, dev, False, warmup=1,
+                                                        iters=int(os.environ.get("MCCS_SETUP2_ITERS", "10"))))
     dist.barrier()
-    if not getattr(args, "no_extra", False) and os.environ.get("MCCS_BENCH_NO_REFDRV") != "1":
-        extras["reference_driven"] = reference_driven_leg(torch, dist, rank, world, device, nbytes)
+    if extra and os.environ.get("MCCS_BENCH_NO_REFDRV") != "1":
+        extras["reference_driven"] = budget.run(
+            "reference_driven", lambda: reference_driven_leg(torch, dist, rank, world, device, nbytes))
     calib = None
-    if not getattr(args, "no_extra", False):
+    if extra and budget.allow("node_legs"):
         # rank 0 alone drives every GPU; ranks 1..N-1 wait at the barrier below
+        t = budget.clock()
         if rank == 0:
             extras["in_process_multi_device"], calib = node_legs(torch, C, world, ndev, nbytes,
                                                                  mode_config(C, mode, info))
             extras["xgmi_calibration"] = calib
         dist.barrier()
+        budget.note("node_legs", t)
+    # every rank decides the CPU ring leg alike (rank 0 runs it; the others wait)
+    cpu_ring = extra and budget.allow("cpu_ring_baseline")
     if rank != 0:
         dist.barrier()  # rank 0 times the host baseline
         return None
     cpu = None
     if not getattr(args, "no_cpu_baseline", False) and cpu_sum_baseline is not None:
+        t = budget.clock()
         cpu = cpu_sum_baseline(world, nbytes, 7)
-        # host threads = world x channels: at most the default channel count
-        # (a doubled-channel transport would double the spinning threads)
-        host_ch = min(info["channels"], len(C.default_rings(world, 0)))
-        extras["cpu_ring_baseline"] = cpu_ring_baseline(world, min(nbytes, 16 << 20), host_ch)
+        budget.note("cpu_baseline", t)
+        if cpu_ring:
+            # host threads = world x channels: at most the default channel count
+            # (a doubled-channel transport would double the spinning threads)
+            host_ch = min(info["channels"], len(C.default_rings(world, 0)))
+            t = budget.clock()
+            extras["cpu_ring_baseline"] = cpu_ring_baseline(world, min(nbytes, 16 << 20), host_ch)
+            budget.note("cpu_ring_baseline", t)
     dist.barrier()
+    extras["budget"] = budget.summary()
     prof = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in prof.items()}
     return ring_line(world=world, steps=K, warmup=args.warmup, per_step_s=per_step, nbytes=nbytes, dt_name=dt_name,
                      comm_info=info, rings=rings, mode=mode, tune_table=tune_table, prof=prof,

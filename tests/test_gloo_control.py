@@ -204,3 +204,46 @@ def test_bench_gate_rejects_a_mode_on_every_rank_and_records_it():
         # m1: U (rejected, destroyed) + D; m2: U skipped, D; m1 again with a fresh list: U + D both
         # rejected; m4: U (rejected) + R
         assert made == 7 and first_destroyed and not c1_destroyed and not c2_destroyed
+
+
+def _budget_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from mccs_amd import ring_bench as rb
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        now = [0.0]
+        b = rb.Budget(dist, seconds=100, clock=lambda: now[0])
+        ran = []
+        b.run("a", lambda: ran.append("a"), need_s=10)
+        now[0] = 95.0 if rank == 0 else 10.0  # only rank 0's clock says a 10 s leg no longer fits
+        b.run("b", lambda: ran.append("b"), need_s=10)
+        now[0] = 96.0 if rank == 0 else 11.0
+        b.run("c", lambda: ran.append("c"), need_s=1)
+        q.put((rank, ran, b.summary()["legs"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_budget_skips_a_leg_on_every_rank():
+    """ring_bench.Budget: the extra legs are collective, so a leg that does not
+    fit the budget on ANY rank's clock is skipped on all of them (recorded as
+    skipped), and a later leg that fits still runs everywhere."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_budget_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ran, legs in res:
+        assert ran == ["a", "c"], (rank, ran)
+        assert legs["b"]["skipped"] == "budget" and legs["b"]["need_s"] == 10
+        assert "wall_s" in legs["a"] and "wall_s" in legs["c"]

@@ -197,3 +197,59 @@ def test_node_legs_report_na_when_ranks_share_a_gpu():
 def test_ring_cpu_baseline_samples_large_buckets():
     cb = bench.ring_cpu_baseline(2, 1 << 30, 6, budget_s=0.2)
     assert "first 256 MiB of the 1024 MiB bucket" in cb["sample"] and cb["value"] > 0
+
+
+class _OneRankDist:
+    """torch.distributed stand-in for a world of one (agree() reduces over it)."""
+
+    class ReduceOp:
+        MIN, MAX = "min", "max"
+
+    @staticmethod
+    def all_reduce(t, op=None, group=None):
+        return None
+
+
+def test_budget_skips_late_legs_and_the_line_keeps_its_headline():
+    """the N > 1 line must survive a slow node.  With a clock
+    that jumps 100 s per leg and a 210 s budget, the first two legs run, the
+    rest are recorded as skipped, and the line still carries value, roofline
+    and cpu_baseline, plus every leg's wall time or skip."""
+    now = [0.0]
+
+    def clock():
+        return now[0]
+
+    b = rb.Budget(_OneRankDist, seconds=210, clock=clock)
+    ran = []
+    for name in ("graph_replay", "configs3_fp16_1GiB", "size_sweep_fp16", "reference_driven", "node_legs"):
+        def leg(name=name):
+            ran.append(name)
+            now[0] += 100.0
+            return {"ok": True}
+        b.run(name, leg)
+    assert ran == ["graph_replay", "configs3_fp16_1GiB"]
+    legs = b.summary()["legs"]
+    assert legs["graph_replay"]["wall_s"] == 100.0
+    for name in ("size_sweep_fp16", "reference_driven", "node_legs"):
+        assert legs[name]["skipped"] == "budget" and legs[name]["at_s"] == 200.0
+    d = rb.ring_line(world=8, steps=20, warmup=5, per_step_s=1.2e-3, nbytes=128 << 20, dt_name="float32",
+                     comm_info={"channels": 7, "lanes": 9, "block_threads": 576}, rings=C.default_rings(8),
+                     mode="receiver-uncached-fifo", tune_table=[], prof={}, ranks_share_gpu=False,
+                     cpu_baseline=bench.ring_cpu_baseline(2, 1 << 20, budget_s=0.2),
+                     extras={"budget": b.summary(), "size_sweep_fp16": None})
+    assert d["value"] > 0 and d["roofline"]["frac"] > 0 and d["cpu_baseline"]["value"] > 0
+    assert d["config"]["budget"]["legs"]["node_legs"]["skipped"] == "budget"
+    assert "size_sweep_fp16" not in d["config"]
+    json.dumps(d)
+
+
+def test_budget_default_and_override(monkeypatch):
+    monkeypatch.delenv("MCCS_BENCH_BUDGET_S", raising=False)
+    assert rb.Budget(_OneRankDist).seconds == rb.DEFAULT_BUDGET_S
+    monkeypatch.setenv("MCCS_BENCH_BUDGET_S", "42")
+    assert rb.Budget(_OneRankDist).seconds == 42.0
+    # every leg the N > 1 run can skip has an expected time
+    for name in ("graph_replay", "configs3_fp16_1GiB", "allgather_16MiB_per_rank", "size_sweep_fp16",
+                 "direct_sweep_fp16", "configs4_two_jobs", "reference_driven", "node_legs", "cpu_ring_baseline"):
+        assert rb.LEG_NEED_S[name] > 0

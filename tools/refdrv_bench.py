@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--mib", type=int, default=128)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rotate-mib", type=int, default=1152,
+                    help="send/recv pairs rotated per rank (>= this many MiB; 0 = one pair reused)")
+    ap.add_argument("--variants", default=None, help="comma-separated variant names (default: all)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -37,12 +40,17 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     max_ch = max(2, 128 // world) if ndev < world else 32  # ranks sharing a GPU: half the CUs
-    res = refdrive.time_reference_driven(torch, dist, rank, world, dev, a.mib << 20,
-                                         refdrive.default_variants(world, C.default_rings, max_ch),
-                                         warmup=a.warmup, steps=a.steps)
+    variants = refdrive.default_variants(world, C.default_rings, max_ch)
+    if a.variants:
+        keep = set(a.variants.split(","))
+        variants = [v for v in variants if v["name"] in keep]
+    res = refdrive.time_reference_driven(torch, dist, rank, world, dev, a.mib << 20, variants,
+                                         warmup=a.warmup, steps=a.steps, rotate_bytes=a.rotate_mib << 20)
     if rank == 0:
         print(json.dumps({"tool": "refdrv_bench", "world": world, "ranks_share_gpu": ndev < world,
-                          "bytes_per_rank": a.mib << 20, "dtype": "f32", "variants": res}), flush=True)
+                          "bytes_per_rank": a.mib << 20, "dtype": "f32", "rotate_mib": a.rotate_mib,
+                          "library": os.environ.get("MCCS_LIB_PATH", "mccs_amd/libmccs_hip.so"),
+                          "variants": res}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -20,7 +20,7 @@
 //         flight, counted vmcnt waits (lds_dma.h)
 // Prints GB/s of HBM traffic per workgroup (loads + stores) per design.
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I mccs_amd/csrc \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I mccs_amd/csrc -I tools \
 //       -o wg_stream tools/wg_stream.hip && ./wg_stream [G] [MiB per WG] [slice KiB]
 #include <hip/hip_runtime.h>
 
@@ -31,6 +31,7 @@
 #include "lds_dma.h"
 #include "reduce_copy.h"
 #include "ring_stream.h"
+#include "wg_stream_rows.h"
 
 #define CK(x)                                                                         \
   do {                                                                                \
@@ -61,7 +62,6 @@ __global__ void __launch_bounds__(576) stream_kernel(const float* s0, const floa
   const int ndthr = (nthr / 64) * 64 == nthr ? nthr - 64 : (nthr / 64) * 64;  // whole waves, minus control
   const int wave = threadIdx.x >> 6;
   const bool data = threadIdx.x < ndthr;
-  const u32x4 none[1] = {};
   for (long off = 0; off < per_wg; off += slice) {
     const long n = slice < per_wg - off ? slice : per_wg - off;
     const float* a = s0 + base + off;
@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(576) stream_kernel(const float* s0, const floa
     float* y = d1 + base + off;
     if (data) {
       if constexpr (DES == 0) {
-        reduce_copy_rows<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr, false, none);
+        reduce_copy_rows<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr);
       } else if constexpr (DES == 1) {
         reduce_copy_rows_pp<mccsFloat32, OpSum, U, NS, ND, NTM, P0, P1>(a, b, x, y, n, threadIdx.x, ndthr);
       } else if constexpr (DES == 3) {
