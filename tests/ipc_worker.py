@@ -22,6 +22,43 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
+def ddp_stream(comm, rank, world, orc, vnode):
+    """Two steps of vnode.DDP_STREAM issued back to back on the library's
+    default routing, one sync at the end; every bucket checked against the
+    oracle and for the kernel the defaults give it."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from mccs_amd import comm as C
+
+    rng = np.random.default_rng(500 + rank)
+    cases = []
+    for step in range(2):
+        for code, nbytes in vnode.DDP_STREAM:
+            x = vnode.gen(code, nbytes // vnode.ESIZE[code], rng)
+            xs = [None] * world
+            dist.all_gather_object(xs, x)
+            cases.append((code, xs, vnode.to_dev(x), vnode.to_dev(np.zeros_like(x))))
+    algos = []
+    for code, xs, send, recv in cases:
+        C.all_reduce(comm, send, recv, xs[0].size, code, 0)
+        algos.append(comm.last_algo())
+    torch.cuda.synchronize()
+    comm.sync()
+    out = {}
+    uncached = comm.fifo_memory != C.FIFO_DEVICE
+    for i, (code, xs, send, recv) in enumerate(cases):
+        p = vnode.Planner(comm.nchannels, comm.rings())
+        nch, nthr, rings = p.select(xs[0].nbytes, 0)
+        exp = orc.ring_allreduce(code, 0, xs, nchannels=nch, nthreads=nthr, ring_orders=rings)
+        got = vnode.from_dev(recv, code)
+        ok = bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8)))
+        want = vnode.ddp_expected_algo(xs[0].nbytes, world, uncached)
+        out[f"ddp/{algos[i]}/b{i}"] = ok and algos[i] == want
+    return out
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -52,7 +89,9 @@ def main():
                  "direct": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
                  "oneshot": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
                  # LL one-shot up to 1 MiB (larger buckets: the one-shot)
-                 "ll": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
+                 "ll": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
+                 # the library defaults, fed a DDP-style bucket stream (vnode.DDP_STREAM)
+                 "ddp": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
     direct_kw = {"direct": dict(direct_bytes=8 << 20, oneshot_bytes=-1, ll_bytes=-1),
                  "oneshot": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=-1),
                  "ll": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=1 << 20)}
@@ -67,6 +106,10 @@ def main():
         comm = C.init_communicator_rank(rank, world, dev, exchange,
                                         C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, lanes=lanes,
                                                      **direct_kw.get(mode, {})))
+        if mode == "ddp":
+            results.update(ddp_stream(comm, rank, world, orc, vnode))
+            comm.destroy()
+            continue
         cases = [(2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)]
         nfuzz = int(os.environ.get("IPC_FUZZ", "0"))
         if nfuzz:  # seeded random dtypes / ragged counts, same on every rank

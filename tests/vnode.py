@@ -84,3 +84,32 @@ def destroy(comms):
     torch.cuda.synchronize()
     for c in comms:
         c.destroy()
+
+
+# A DDP-style bucket stream (tests/test_gpu_ddp_stream.py, tests/ipc_worker.py
+# "ddp"): (dtype code, bytes per rank) of one step's buckets -- a small first
+# bucket, DDP's 25 MiB buckets, ragged remainders, and sizes on both sides of
+# every default direct / LL threshold.
+DDP_STREAM = [(7, 24), (6, 16 << 10), (7, 100 << 10), (9, (128 << 10) + 2), (7, 200 << 10),
+              (6, 600 << 10), (7, 1 << 20), (7, (1 << 20) + 4), (6, 1536 << 10), (7, 2 << 20),
+              (7, 3 << 20), (6, 6 << 20), (7, 8 << 20), (7, (8 << 20) + 4096), (7, 25 << 20),
+              (6, 25 << 20), (7, (7 << 20) + 12)]
+
+
+def ddp_expected_algo(nbytes: int, n: int, uncached: bool = True) -> str:
+    """The kernel the library's defaults give a bucket of nbytes per rank
+    (api.cpp fill_defaults; LL needs an uncached arena; peer atomics assumed)."""
+    import ctypes
+
+    from mccs_amd import _lib
+
+    lib = _lib.load()
+    one, two = ctypes.c_int(), ctypes.c_int()
+    lib.mccs_direct_defaults(n, ctypes.byref(one), ctypes.byref(two))
+    if uncached and nbytes <= lib.mccs_ll_default(n):
+        return "ll"
+    if one.value > 0 and nbytes <= one.value:
+        return "oneshot"
+    if two.value > 0 and nbytes <= two.value:
+        return "direct"
+    return "ring"
