@@ -53,6 +53,9 @@ void err_clear() {
 }
 
 void err_hip(const char* call, hipError_t e, const char* file, int line) {
+  // the failure travels in the result and this record; no sticky copy stays
+  // on the thread for the caller's next hipGetLastError() to find
+  (void)hipGetLastError();
   char buf[512];
   std::snprintf(buf, sizeof(buf), "%s: %s -> %s (%s) at %s:%d", step_path().c_str(), call_name(call).c_str(),
                 hipGetErrorName(e), hipGetErrorString(e), base_name(file), line);
