@@ -265,3 +265,26 @@ def test_fused_comm_sync_does_not_hold_the_live_lock(lib):
         lib.mccs_test_fake_delay(None, 0)
         for c in comms:
             c.destroy()
+
+
+def test_init_all_failure_names_the_rank_and_step(lib):
+    """mccsCommInitAll (one process driving every GPU): a failure in the
+    second rank's setup names that rank and step, and frees the first rank."""
+    _fresh(lib)
+    lib.mccs_test_fake_fail(b"HostMallocMapped", 4, OOM)  # rank 1's work FIFO (3 per rank)
+    comms = (ctypes.c_void_p * 2)()
+    devs = (ctypes.c_int * 2)(0, 1)
+    cfg, keep = C.CommConfig().to_c(2)
+    rc = lib.mccsCommInitAll(comms, 2, devs, ctypes.byref(cfg))
+    err = lib.mccsGetLastErrorString().decode()
+    assert rc == 1
+    assert err.startswith("mccsCommInitAll(2 ranks) > rank 1 > comm_alloc_local > work FIFO: HostMallocMapped -> "
+                          "hipErrorOutOfMemory"), err
+    blocks, events, pooled = _live(lib)
+    assert events == 0 and blocks == pooled == 2, (blocks, events, pooled)
+    # a clean init clears the record
+    _fresh(lib)
+    assert lib.mccsCommInitAll(comms, 2, devs, ctypes.byref(cfg)) == 0
+    assert lib.mccsGetLastErrorString() == b""
+    for h in comms:
+        lib.mccsCommDestroy(h)
