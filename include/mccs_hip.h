@@ -197,6 +197,11 @@ mccsResult_t mccsGroupEnd(void);
 mccsResult_t mccsCommSync(mccsComm_t comm);
 /* Raises the comm's abortFlag: in-flight kernels exit at their next poll. */
 mccsResult_t mccsCommAbort(mccsComm_t comm);
+/* Frees the comm.  Across processes, destroy only after every rank's last
+ * collective has completed (mccsCommSync on every rank, then an out-of-band
+ * barrier): a peer's last flag post can land in this rank's FIFO arena after
+ * this rank's own kernel finished, and the arena goes back to a per-process
+ * pool that the next communicator of the same size reuses. */
 mccsResult_t mccsCommDestroy(mccsComm_t comm);
 /* rank, nranks, device, channels, lanes, block threads, fifo memory kind
  * (MCCS_FIFO_*: the hand-off mode the comm's launches run). */

@@ -555,6 +555,9 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
     try:
         torch.cuda.synchronize()
     finally:
+        # every rank's last kernel is done before any arena returns to the pool
+        # (mccsCommDestroy contract, include/mccs_hip.h)
+        dist.barrier()
         for cm in comms.values():
             try:
                 cm.destroy()
@@ -987,8 +990,11 @@ def setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup
     for it in range(iters):
         tj.iteration(it)
     ok = all(r.exact for r in tj.records)
-    comm.destroy()
-    require(dist, ok, f"{name}: in-place exact-sum check of every iteration")
+    try:
+        # the all-rank agreement doubles as the barrier mccsCommDestroy needs
+        require(dist, ok, f"{name}: in-place exact-sum check of every iteration")
+    finally:
+        comm.destroy()
     mine = tj.summary()
     mine["fifo_mode"] = mode
     # per-job numbers as the max over the job's ranks (the slowest rank ends the op)

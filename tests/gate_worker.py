@@ -106,6 +106,7 @@ def main():
             comm.sync()
             results[f"{name}/{nbytes}"] = {"ok": bool(torch.equal(recv, want)) and comm.last_algo() == algo,
                                            "algo": comm.last_algo()}
+        dist.barrier()  # every rank's last kernel is done before any arena returns to the pool
         comm.destroy()
     allres = [None] * world
     dist.all_gather_object(allres, results)

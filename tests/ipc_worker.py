@@ -108,6 +108,7 @@ def main():
                                                      **direct_kw.get(mode, {})))
         if mode == "ddp":
             results.update(ddp_stream(comm, rank, world, orc, vnode))
+            dist.barrier()  # every rank's last kernel is done before any arena returns to the pool
             comm.destroy()
             continue
         cases = [(2, 1 << 20), (7, 300007), (6, 1000003), (9, 77777), (7, 3)]
@@ -172,6 +173,7 @@ def main():
             auto = (128 if world == 2 else 64) // comm.nchannels
             want = min(auto, 256 // 2 // (world * comm.nchannels))
             results[f"{mode}/colocated_lanes={comm.lanes}"] = comm.lanes == want
+        dist.barrier()  # every rank's last kernel is done before any arena returns to the pool
         comm.destroy()
     allres = [None] * world
     dist.all_gather_object(allres, results)
