@@ -253,3 +253,35 @@ def test_budget_default_and_override(monkeypatch):
     for name in ("graph_replay", "configs3_fp16_1GiB", "allgather_16MiB_per_rank", "size_sweep_fp16",
                  "direct_sweep_fp16", "configs4_two_jobs", "reference_driven", "node_legs", "cpu_ring_baseline"):
         assert rb.LEG_NEED_S[name] > 0
+
+
+def test_scale_report_reads_a_node_line(tmp_path):
+    """tools/scale_report.py (the round-6 reading of the first SCALE record)
+    finds N > 1 lines at any nesting and reports gate, roofline, autotune,
+    depth A and budget."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "scale_report", os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "scale_report.py"))
+    sr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sr)
+    b = rb.Budget(_OneRankDist, seconds=10, clock=lambda: 0.0)
+    b.legs = {"headline": {"wall_s": 1.5}, "size_sweep_fp16": {"skipped": "budget", "at_s": 9.0, "need_s": 25}}
+    d = rb.ring_line(world=8, steps=20, warmup=5, per_step_s=1.2e-3, nbytes=128 << 20, dt_name="float32",
+                     comm_info={"channels": 7, "lanes": 9, "block_threads": 576}, rings=C.default_rings(8),
+                     mode="receiver-uncached-fifo",
+                     tune_table=[{"mode": "receiver-uncached-fifo", "channels": 7, "lanes": 9, "ms_per_step": 1.2}],
+                     prof={}, ranks_share_gpu=False, cpu_baseline=None,
+                     extras={"budget": b.summary(),
+                             "node_gate": {"ran": True, "fifo_memory_run": 2, "failed_bits": 0x1, "disabled_bits": 0x8},
+                             "rejected_before_timing": [{"mode": "sender-uncached-fifo", "rank0_reason": "exact-sum mismatch"}],
+                             "connect_timing_per_rank": [{"setup_s": 0.1, "exchange_s": 0.2, "connect_s": 1.5}]})
+    p = tmp_path / "scale.json"
+    p.write_text(json.dumps({"runs": {"8": d}, "1": {"metric": "x", "n_gpus": 1, "config": {}}}))
+    lines = [l for line in sr.load(str(p)) for l in sr.report(line)]
+    text = "\n".join(lines)
+    assert "N = 8" in text and "N = 1" not in text
+    assert "hand-off=uncached + release" in text and "failed=[ring uncached]" in text and "disabled=[LL]" in text
+    assert "stepped down" in text and "rejected before timing: sender-uncached-fifo (exact-sum mismatch)" in text
+    assert "skipped ['size_sweep_fp16']" in text and "slowest connect (+ gate): 1.5 s" in text
