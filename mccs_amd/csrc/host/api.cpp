@@ -182,28 +182,37 @@ static mccsResult_t enable_peer(int a, int b) {
 
 static mccsResult_t launch_single(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count,
                                   hipStream_t stream) {
-  err_clear();
-  auto reject = [](mccsResult_t e) {
-    if (g_group.depth > 0 && g_group.error == mccsSuccess) g_group.error = e;
+  // inside a group the diagnosis of a rejected call must survive to GroupEnd
+  // (the group was cleared at GroupStart)
+  if (g_group.depth == 0) err_clear();
+  auto reject = [](mccsResult_t e, const char* why) {
+    const bool first = g_group.depth == 0 || g_group.error == mccsSuccess;  // a group keeps its first failure
+    if (g_group.depth > 0 && first) g_group.error = e;
+    if (first) err_note(__FILE__, __LINE__, "%s", why);
     return e;
   };
-  if (!c || !c->connected) return reject(mccsInvalidUsage);
-  if (c->failed) return reject(mccsRemoteError);
+  if (!c || !c->connected) return reject(mccsInvalidUsage, "the communicator is not connected");
+  if (c->failed) return reject(mccsRemoteError, "the communicator failed earlier (watchdog or abort): destroy it");
   if (count == 0) return mccsSuccess;
-  if (!send || !recv) return reject(mccsInvalidArgument);
+  if (!send || !recv) return reject(mccsInvalidArgument, "null send or recv buffer");
   if (func == mccsFuncAllReduce && (dtype < 0 || dtype >= mccsNumTypes || op < 0 || op > mccsDevMin))
-    return reject(mccsInvalidArgument);
+    return reject(mccsInvalidArgument, "unknown dtype or reduction op");
   if (std::find(g_group.comms.begin(), g_group.comms.end(), c) == g_group.comms.end()) {
     g_group.comms.push_back(c);
     g_group.streams.push_back(stream);
   }
-  mccsResult_t er = plan_enqueue(c, func, dtype, op, send, recv, count);
+  mccsResult_t er;
+  {
+    StepScope st(func == mccsFuncAllGather ? "mccsAllGather" : "mccsAllReduce");
+    er = plan_enqueue(c, func, dtype, op, send, recv, count);
+  }
   if (er != mccsSuccess) {
     if (g_group.depth == 0) group_discard();
     else if (g_group.error == mccsSuccess) g_group.error = er;
     return er;
   }
   if (g_group.depth == 0) {
+    StepScope st(func == mccsFuncAllGather ? "mccsAllGather launch" : "mccsAllReduce launch");
     mccsResult_t r = plan_launch_group(g_group.comms, g_group.streams);
     group_discard();
     return r;
@@ -534,13 +543,15 @@ extern "C" mccsResult_t mccsAllGather(const void* sendbuff, void* recvbuff, size
 }
 
 extern "C" mccsResult_t mccsGroupStart(void) {
-  ++g_group.depth;
+  if (g_group.depth++ == 0) err_clear();
   return mccsSuccess;
 }
 
 extern "C" mccsResult_t mccsGroupEnd(void) {
-  err_clear();
-  if (g_group.depth <= 0) return mccsInvalidUsage;
+  if (g_group.depth <= 0) {
+    err_clear();
+    MCCS_FAIL(mccsInvalidUsage, "mccsGroupEnd without mccsGroupStart");
+  }
   if (--g_group.depth > 0) return mccsSuccess;
   if (g_group.error != mccsSuccess) {  // a collective of the group was rejected: launch none
     const mccsResult_t e = g_group.error;
@@ -548,6 +559,7 @@ extern "C" mccsResult_t mccsGroupEnd(void) {
     group_discard();
     return e;
   }
+  StepScope st("mccsGroupEnd launch");
   mccsResult_t r = plan_launch_group(g_group.comms, g_group.streams);
   group_discard();  // plans not launched after an error are dropped, not left queued
   return r;

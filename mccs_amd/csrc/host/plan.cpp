@@ -119,7 +119,8 @@ static bool ll_fits(const Comm* c, size_t bytes) {
 
 mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count) {
   if (c->plan_pending && (c->plan_func != func || c->plan_dtype != dtype || c->plan_op != op))
-    return mccsInvalidUsage;  // pre_launch_schedule batches same func/dtype/op only (plan.rs:122-141)
+    // pre_launch_schedule batches same func/dtype/op only (plan.rs:122-141)
+    MCCS_FAIL(mccsInvalidUsage, "a group mixes collectives of different function / dtype / op on one communicator");
   MCCS_CHECK(demote_direct(c));
   // One AllReduce that fits the direct region (every rank decides alike: same
   // call, same config) is held for the direct kernel; the launch may still
@@ -185,7 +186,7 @@ static mccsResult_t wait_work_queue(Comm* c, uint32_t target) {
     if (!rolling_less_u32(c->work_acked_min + c->work_depth, target)) return mccsSuccess;
     if ((spins & 0xfffff) == 0xfffff && rt().EventQuery(c->event) == hipSuccess) {
       // stream idle but acks missing: the kernel aborted
-      return mccsRemoteError;
+      MCCS_FAIL(mccsRemoteError, "work FIFO full and its kernel no longer running (aborted or timed out)");
     }
     sched_yield();
   }
@@ -225,10 +226,9 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld) {
       work_count += (uint32_t)c->sched[ch].works.size();
     }
   if (chan_list.empty()) return mccsInternalError;
-  if (c->graph_work_used + work_count > Comm::kGraphWorkEntries) {
-    MCCS_LOG("graph work arena exhausted (%u of %u entries used)", c->graph_work_used, Comm::kGraphWorkEntries);
-    return mccsInvalidUsage;
-  }
+  if (c->graph_work_used + work_count > Comm::kGraphWorkEntries)
+    MCCS_FAIL(mccsInvalidUsage, "graph work arena exhausted (%u of %u entries used)", c->graph_work_used,
+              Comm::kGraphWorkEntries);
   mccsDevWork* head = c->h_graph_work + c->graph_work_used;
   const uint32_t nchan = (uint32_t)chan_list.size();
   uint32_t subsequent = nchan;
@@ -542,11 +542,9 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   if (idx.size() > 1) g = std::min<long>(g, std::min(cap, ncu) / (long)idx.size());  // one fused launch
   else if (c0->share > 1) g = std::min<long>(g, std::min(cap / 2, ncu) / c0->share);  // separate processes
   g = std::max<long>(g, 1);
-  if (g * (long)idx.size() > cap) {
-    MCCS_LOG("direct launch of %zu ranks x %ld workgroups exceeds the %d co-resident ones of device %d", idx.size(),
-             g, cap, c0->device);
-    return mccsInvalidUsage;
-  }
+  if (g * (long)idx.size() > cap)
+    MCCS_FAIL(mccsInvalidUsage, "direct launch of %zu ranks x %ld workgroups exceeds the %d co-resident ones of device %d",
+              idx.size(), g, cap, c0->device);
   *grid_x = (unsigned)g;
   auto piece = [&](size_t phase_bytes) {
     size_t p = (phase_bytes + (size_t)g - 1) / (size_t)g;
@@ -587,9 +585,9 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       const int cap = coresident_ring_blocks(c0->block_threads, kv.first);
       const long need = (long)c0->nch * c0->lanes * (long)idx.size();
       if (need > cap) {
-        MCCS_LOG("fused launch of %zu ranks x %d blocks exceeds the %d co-resident blocks of device %d",
-                 idx.size(), c0->nch * c0->lanes, cap, kv.first);
-        return mccsInvalidUsage;  // would deadlock: every block spins on a peer's flag
+        // would deadlock: every block spins on a peer's flag
+        MCCS_FAIL(mccsInvalidUsage, "fused launch of %zu ranks x %d blocks exceeds the %d co-resident blocks of device %d",
+                  idx.size(), c0->nch * c0->lanes, cap, kv.first);
       }
     }
     // A capturing stream records this launch into a HIP graph: its work
@@ -625,7 +623,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       // Communicator launches carry their hand-off policy in the arguments
       // (one launch per device; blockIdx.y = rank slot when ranks share it).
       // Fused ranks take the safest policy of the group.
-      if (idx.size() > MCCS_MULTI_MAX_RANKS) return mccsInvalidUsage;
+      if (idx.size() > MCCS_MULTI_MAX_RANKS)
+        MCCS_FAIL(mccsInvalidUsage, "%zu ranks share one device (at most %d)", idx.size(), (int)MCCS_MULTI_MAX_RANKS);
       ma.channelMask = lds[0].mask;
       ma.cfg = c0->kcfg;
       for (size_t k = 0; k < idx.size(); ++k) {
@@ -633,7 +632,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
         if (lds[k].mask != lds[0].mask || lds[k].multi_fn != lds[0].multi_fn || ck->lanes != c0->lanes ||
             ck->block_threads != c0->block_threads || ck->kcfg.slice_steps != c0->kcfg.slice_steps ||
             ck->kcfg.fifo_slots != c0->kcfg.fifo_slots)
-          return mccsInvalidUsage;  // ranks sharing a GPU must issue the same collective
+          MCCS_FAIL(mccsInvalidUsage, "ranks sharing a GPU issued different collectives in one group");
         ma.comm[k] = (mccsDevComm*)ck->d_comm;
         ma.work[k] = lds[k].work;
         ma.view[k] = ck->d_view;

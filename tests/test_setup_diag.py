@@ -288,3 +288,36 @@ def test_init_all_failure_names_the_rank_and_step(lib):
     assert lib.mccsGetLastErrorString() == b""
     for h in comms:
         lib.mccsCommDestroy(h)
+
+
+def test_group_keeps_the_first_rejection(lib):
+    """A collective rejected inside a group fails the whole group at
+    mccsGroupEnd; the diagnosis of that first rejection survives the later
+    calls of the group (they no longer clear it)."""
+    _fresh(lib, 1)
+    comms = C.init_all([0, 0])
+    try:
+        assert lib.mccsGroupStart() == 0
+        assert lib.mccsAllReduce(ctypes.c_void_p(0x1000), ctypes.c_void_p(0x2000), 64, 77, 0, comms[0]._h, None) == 4
+        assert lib.mccsAllReduce(ctypes.c_void_p(0x1000), ctypes.c_void_p(0x2000), 64, 7, 0, comms[1]._h, None) == 0
+        assert lib.mccsGroupEnd() == 4
+        err = lib.mccsGetLastErrorString().decode()
+        assert "unknown dtype or reduction op" in err, err
+        # mixing collectives of one communicator in a group is refused by the planner, with its reason
+        assert lib.mccsGroupStart() == 0
+        assert lib.mccsAllReduce(ctypes.c_void_p(0x1000), ctypes.c_void_p(0x2000), 64, 7, 0, comms[0]._h, None) == 0
+        rc = lib.mccsAllReduce(ctypes.c_void_p(0x1000), ctypes.c_void_p(0x2000), 64, 6, 0, comms[0]._h, None)
+        assert rc == 5
+        assert lib.mccsGroupEnd() == 5
+        err = lib.mccsGetLastErrorString().decode()
+        assert err.startswith("mccsAllReduce: a group mixes collectives"), err
+        # a clean call clears it
+        with C.group():
+            for r, c in enumerate(comms):
+                C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 64, 7, 0, stream=0)
+        assert lib.mccsGetLastErrorString() == b""
+        assert lib.mccsGroupEnd() == 5  # without a start
+        assert "mccsGroupEnd without mccsGroupStart" in lib.mccsGetLastErrorString().decode()
+    finally:
+        for c in comms:
+            c.destroy()
