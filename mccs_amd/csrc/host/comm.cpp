@@ -134,12 +134,16 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
   return mccsSuccess;
 }
 
-// Process-wide FIFO arena pool.  Arenas are never returned to the runtime:
-// on this ROCm stack a virtual range freed as one memory type (coarse device
-// memory) and re-allocated as another (uncached) kept behaving like the old
-// type inside kernels (stale translations), corrupting FIFO hand-offs.
-// Pooling by (device, type, size) means the library never flips the type of
-// a range it owns.
+// Process-wide FIFO arena pool.  Arenas are not returned to the runtime while
+// the device has memory: on this ROCm stack a virtual range freed as one memory
+// type (coarse device memory) and re-allocated as another (uncached) kept
+// behaving like the old type inside kernels (stale translations), corrupting
+// FIFO hand-offs.  Pooling by (device, type) means the library never flips the
+// type of a range it owns.  Requests round up to a size class and take the
+// smallest pooled arena of at least that size (at most twice it), so
+// communicators of nearby shapes share arenas and a process that creates many
+// shapes does not keep one arena per shape (a 2,000-case fuzz on one GPU ran
+// out of HBM at case 876 with exact-size pooling).
 struct PooledArena {
   unsigned generation;  // rt_generation() of the runtime that allocated it
   int device;
@@ -150,21 +154,77 @@ struct PooledArena {
 static std::mutex g_pool_mu;
 static std::vector<PooledArena> g_pool;
 
-static char* pool_take(int device, bool uncached, size_t bytes) {
+// need rounded up to a quarter of its power of two (64 KiB granule at least):
+// at most 25 % over, a few dozen classes between 1 MiB and 4 GiB
+static size_t arena_class(size_t need) {
+  size_t q = (size_t)1 << 16;
+  while (q * 2 <= need) q <<= 1;
+  const size_t g = std::max<size_t>((size_t)1 << 16, q / 4);
+  return (need + g - 1) / g * g;
+}
+
+static char* pool_take(int device, bool uncached, size_t need, size_t* got) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  for (size_t i = 0; i < g_pool.size(); ++i)
-    if (g_pool[i].generation == rt_generation() && g_pool[i].device == device && g_pool[i].uncached == uncached &&
-        g_pool[i].bytes == bytes) {
-      char* p = g_pool[i].ptr;
-      g_pool.erase(g_pool.begin() + i);
-      return p;
-    }
-  return nullptr;
+  size_t best = g_pool.size();
+  for (size_t i = 0; i < g_pool.size(); ++i) {
+    const PooledArena& a = g_pool[i];
+    if (a.generation == rt_generation() && a.device == device && a.uncached == uncached && a.bytes >= need &&
+        a.bytes <= 2 * need && (best == g_pool.size() || a.bytes < g_pool[best].bytes))
+      best = i;
+  }
+  if (best == g_pool.size()) return nullptr;
+  char* p = g_pool[best].ptr;
+  *got = g_pool[best].bytes;
+  g_pool.erase(g_pool.begin() + best);
+  return p;
 }
 
 static void pool_give(int device, bool uncached, size_t bytes, char* p) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
   g_pool.push_back(PooledArena{rt_generation(), device, uncached, bytes, p});
+}
+
+// Out of device memory: return this device's pooled uncached arenas to the
+// runtime (no live communicator uses them).  Only uncached ones: whatever
+// re-allocates such a range at worst sees uncached behaviour, which is still
+// correct; a freed coarse range re-allocated as an uncached arena is the case
+// the pool exists to avoid.  Returns the bytes released.
+static size_t pool_release_uncached(int device) {
+  std::vector<char*> drop;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size();)
+      if (g_pool[i].generation == rt_generation() && g_pool[i].device == device && g_pool[i].uncached) {
+        drop.push_back(g_pool[i].ptr);
+        bytes += g_pool[i].bytes;
+        g_pool.erase(g_pool.begin() + i);
+      } else {
+        ++i;
+      }
+  }
+  for (char* p : drop) (void)rt().Free(p);
+  if (!drop.empty()) MCCS_LOG("device %d out of memory: released %zu pooled FIFO arenas (%zu bytes)", device,
+                              drop.size(), bytes);
+  return bytes;
+}
+
+// A FIFO arena of at least `need` bytes and the given type on the current
+// device: a pooled one if one fits, else a new allocation of need's size
+// class, retried once after releasing the pooled uncached arenas when the
+// device is out of memory.
+static hipError_t arena_alloc(int device, bool uncached, size_t need, char** p, size_t* got) {
+  if ((*p = pool_take(device, uncached, need, got))) return hipSuccess;
+  const size_t bytes = arena_class(need);
+  auto alloc = [&] { return uncached ? rt().MallocUncached((void**)p, bytes) : rt().Malloc((void**)p, bytes); };
+  hipError_t e = alloc();
+  if (e == hipErrorOutOfMemory && pool_release_uncached(device) > 0) e = alloc();
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return e;
+  }
+  *got = bytes;
+  return hipSuccess;
 }
 
 // A fake runtime's "device" memory dies with it (rt.cpp): its pooled arenas
@@ -202,10 +262,16 @@ mccsResult_t comm_switch_to_device_arena(Comm* c) {
   StepScope st("device arena fallback");
   DeviceGuard g(c->device);
   const size_t bytes = c->layout.total();
-  if (c->own_arena) pool_give(c->device, c->own_arena_uncached, bytes, c->own_arena);
+  if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->own_arena_bytes, c->own_arena);
+  c->own_arena = nullptr;
   c->own_arena_uncached = false;
-  c->own_arena = pool_take(c->device, false, bytes);
-  if (!c->own_arena) MCCS_HIP(rt().Malloc((void**)&c->own_arena, bytes));
+  {
+    const hipError_t e = arena_alloc(c->device, false, bytes, &c->own_arena, &c->own_arena_bytes);
+    if (e != hipSuccess) {
+      err_hip("Malloc", e, __FILE__, __LINE__);
+      return mccsUnhandledCudaError;
+    }
+  }
   MCCS_HIP(rt().Memset(c->own_arena, 0, bytes));
   MCCS_HIP(rt().FlushCaches());
   MCCS_HIP(rt().DeviceSynchronize());
@@ -239,22 +305,18 @@ mccsResult_t comm_alloc_local(Comm* c) {
   {
     StepScope st("FIFO arena");
     if (c->cfg.fifo_memory != MCCS_FIFO_DEVICE) {  // UNCACHED or UNCACHED_RELEASE
-      c->own_arena = pool_take(c->device, true, bytes);
-      if (c->own_arena) {
+      const hipError_t e = arena_alloc(c->device, true, bytes, &c->own_arena, &c->own_arena_bytes);
+      if (e == hipSuccess)
         c->own_arena_uncached = true;
-      } else {
-        hipError_t e = rt().MallocUncached((void**)&c->own_arena, bytes);
-        if (e == hipSuccess) {
-          c->own_arena_uncached = true;
-        } else {
-          MCCS_LOG("uncached FIFO arena unavailable (%s); using hipMalloc + system fences", hipGetErrorString(e));
-          c->own_arena = nullptr;
-        }
-      }
+      else
+        MCCS_LOG("uncached FIFO arena unavailable (%s); using hipMalloc + system fences", hipGetErrorString(e));
     }
     if (!c->own_arena) {
-      c->own_arena = pool_take(c->device, false, bytes);
-      if (!c->own_arena) MCCS_HIP(rt().Malloc((void**)&c->own_arena, bytes));
+      const hipError_t e = arena_alloc(c->device, false, bytes, &c->own_arena, &c->own_arena_bytes);
+      if (e != hipSuccess) {
+        err_hip("Malloc", e, __FILE__, __LINE__);
+        return mccsUnhandledCudaError;
+      }
     }
     // trust but verify: the runtime must report the uncached allocation flag
     if (c->own_arena_uncached && !rt().IsUncached(c->own_arena)) {
@@ -455,7 +517,7 @@ mccsResult_t comm_free(Comm* c) {
   if (c->stream) (void)rt().StreamSynchronize(c->stream);
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
     if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)rt().IpcCloseMemHandle(c->peer_arena[r]);
-  if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->layout.total(), c->own_arena);
+  if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->own_arena_bytes, c->own_arena);
   for (auto p : c->d_peers)
     if (p) (void)rt().Free(p);
   for (auto p : c->d_user_ranks)

@@ -157,6 +157,7 @@ struct Comm {
   ArenaLayout layout;
   // arena: own + mapped peers (index by rank); own_arena is peer_arena[rank]
   char* own_arena = nullptr;
+  size_t own_arena_bytes = 0;  // the allocation (its size class), >= layout.total()
   bool own_arena_uncached = true;
   std::vector<char*> peer_arena;
   std::vector<bool> peer_opened_ipc;

@@ -144,7 +144,10 @@ def main():
                 # a hipMalloc arena + system fences on every rank, api.cpp
                 # mccsCommSetupRank) the bucket takes the one-shot instead
                 ll_ok = comm.fifo_memory != C.FIFO_DEVICE
-                want = "oneshot" if mode == "ll" and (count * vnode.ESIZE[code] > 1 << 20 or not ll_ok) else mode
+                nb = count * vnode.ESIZE[code]
+                # above every direct threshold (8 MiB here; IPC_FUZZ draws up to 3M elements) the ring
+                want = ("ring" if nb > 8 << 20 else
+                        "oneshot" if mode == "ll" and (nb > 1 << 20 or not ll_ok) else mode)
                 ok = ok and comm.last_algo() == want
             results[f"{mode}/dtype{code}/n{count}"] = ok
         if mode in direct_kw:  # several launches back to back, fresh inputs each, then one sync

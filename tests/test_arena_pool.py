@@ -1,0 +1,98 @@
+"""The process-wide FIFO arena pool (csrc/host/comm.cpp), on the fake runtime.
+
+Arenas are pooled by (device, memory type) instead of freed, so the library
+never re-allocates a range it owns as another memory type.
+Exact-size pooling kept one arena per communicator shape: a 2,000-case ring
+fuzz (every case a new shape) ran one MI355X out of memory at case 876.  Now a
+request rounds up to a size class and takes the smallest pooled arena of at
+least that size (at most twice it), and an allocation the device refuses for
+lack of memory releases the pooled uncached arenas and retries once.
+"""
+import ctypes
+
+import pytest
+
+from mccs_amd import _lib
+from mccs_amd import comm as C
+
+OOM = 2  # hipErrorOutOfMemory
+
+
+@pytest.fixture
+def lib(monkeypatch):
+    lib = _lib.load()
+    monkeypatch.setenv("MCCS_TEST_HOOKS", "1")
+    monkeypatch.setenv("MCCS_GATE", "0")
+    lib.mccs_test_fake_fail.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    assert lib.mccs_test_fake_runtime(0) == 0
+    assert lib.mccs_test_fake_runtime(2) == 0
+    yield lib
+    lib.mccs_test_fake_runtime(0)
+
+
+def _calls(lib):
+    n = lib.mccs_test_fake_calls(None, 0, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib.mccs_test_fake_calls(buf, n + 1, 1)
+    return [x for x in buf.value.decode().splitlines() if x]
+
+
+def _pooled(lib):
+    b, e, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert lib.mccs_test_fake_live(ctypes.byref(b), ctypes.byref(e), ctypes.byref(p)) == 0
+    return p.value
+
+
+def _cycle(lib, **cfg):
+    """Creates and destroys a 2-rank communicator; returns the arena
+    allocations it made (MallocUncached calls)."""
+    _calls(lib)
+    comms = C.init_all([0, 1], C.CommConfig(**cfg))
+    n = _calls(lib).count("MallocUncached")
+    for c in comms:
+        c.destroy()
+    return n
+
+
+def test_nearby_shapes_share_pooled_arenas(lib):
+    # ring only (no direct slots): arena = flags + channels x 2 x buffer_size
+    base = dict(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1)
+    assert _cycle(lib, channel_count=4, **base) == 2
+    assert _pooled(lib) == 2
+    # the same shape again and a smaller one (within 2x) reuse them
+    assert _cycle(lib, channel_count=4, **base) == 0
+    assert _cycle(lib, channel_count=3, **base) == 0
+    assert _pooled(lib) == 2
+    # a much smaller shape does not pin a 4x larger arena: new allocations
+    assert _cycle(lib, channel_count=1, **base) == 2
+    assert _pooled(lib) == 4
+
+
+def test_many_shapes_keep_the_pool_bounded(lib):
+    """Sixty distinct ring shapes, created and destroyed one after another,
+    leave a handful of pooled arenas, not one per shape."""
+    shapes = [dict(channel_count=ch, buffer_size=bs, fifo_slots=fs, direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1)
+              for ch in (1, 2, 3, 4, 5, 6) for bs in (1 << 20, 3 << 19, 1 << 21, 5 << 19, 1 << 22)
+              for fs in (16, 32)]
+    allocs = sum(_cycle(lib, **s) for s in shapes)
+    assert allocs <= 30 and _pooled(lib) == allocs, (allocs, _pooled(lib))
+
+
+def test_out_of_memory_releases_pooled_uncached_arenas(lib):
+    base = dict(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1)
+    _cycle(lib, channel_count=1, **base)
+    assert _pooled(lib) == 2
+    # a shape no pooled arena fits, on a device that is out of memory: the
+    # pooled arenas go back to the runtime and the allocation is retried
+    assert lib.mccs_test_fake_fail(b"MallocUncached", 1, OOM) == 0
+    _calls(lib)
+    comms = C.init_all([0, 1], C.CommConfig(channel_count=6, **base))
+    trace = _calls(lib)
+    assert trace.count("MallocUncached") == 3, trace  # rank 0: refused, retried; rank 1
+    i = trace.index("MallocUncached")
+    assert "Free" in trace[i:trace.index("MallocUncached", i + 1)], trace
+    assert all(c.fifo_memory == C.FIFO_UNCACHED for c in comms), "the retry must keep the uncached arena"
+    assert _pooled(lib) == 1  # device 0's went back; device 1 had memory
+    for c in comms:
+        c.destroy()
+    assert _pooled(lib) == 3
