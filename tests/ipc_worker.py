@@ -59,6 +59,67 @@ def ddp_stream(comm, rank, world, orc, vnode):
     return out
 
 
+def seq_stream(comm, rank, world, orc, vnode, nops=40):
+    """tests/test_gpu_sequence_fuzz.py's random collective sequence (same
+    list on every rank), issued back to back on this rank's communicator at
+    the library's default routing, one sync at the end, every output checked
+    against the oracle."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from mccs_amd import comm as C
+    from test_gpu_sequence_fuzz import _int_allreduce, sequence
+
+    seq = sequence(np.random.default_rng(9000 + world), nops)
+    rng = np.random.default_rng(77 + rank)
+
+    def gathered(x):
+        xs = [None] * world
+        dist.all_gather_object(xs, x)
+        return xs
+
+    checks, algos = [], set()
+    for i, o in enumerate(seq):
+        if o["kind"] == "ar":
+            x = vnode.gen(o["code"], o["count"], rng)
+            xs = gathered(x)
+            send = vnode.to_dev(x)
+            recv = send if o["inplace"] else vnode.to_dev(np.zeros_like(x))
+            C.all_reduce(comm, send, recv, o["count"], o["code"], o["op"])
+            algos.add(comm.last_algo())
+            p = vnode.Planner(comm.nchannels, comm.rings())
+            nch, nthr, rings = p.select(x.nbytes, 0)
+            exp = orc.ring_allreduce(o["code"], o["op"], xs, nchannels=nch, nthreads=nthr, ring_orders=rings)
+            checks.append((f"{i}/ar/code{o['code']}/op{o['op']}/n{o['count']}", recv, exp, o["code"]))
+        elif o["kind"] == "ag":
+            x = rng.integers(0, 256, o["nbytes"], dtype=np.uint8)
+            xs = gathered(x)
+            send = vnode.to_dev(x)
+            recv = vnode.to_dev(np.zeros(world * o["nbytes"], np.uint8))
+            C.all_gather(comm, send, recv, o["nbytes"])
+            checks.append((f"{i}/ag/b{o['nbytes']}", recv, orc.ring_allgather(xs), None))
+        else:
+            batch = []
+            for count in o["counts"]:
+                x = vnode.gen(o["code"], count, rng)
+                batch.append((count, gathered(x), vnode.to_dev(x), vnode.to_dev(np.zeros_like(x))))
+            with C.group():
+                for count, xs, send, recv in batch:
+                    C.all_reduce(comm, send, recv, count, o["code"], o["op"])
+            for k, (count, xs, send, recv) in enumerate(batch):
+                checks.append((f"{i}.{k}/group/code{o['code']}/op{o['op']}/n{count}", recv,
+                               _int_allreduce(xs, o["op"]), o["code"]))
+    torch.cuda.synchronize()
+    comm.sync()
+    out = {}
+    for what, t, exp, code in checks:
+        got = t.cpu().numpy() if code is None else vnode.from_dev(t, code)
+        out[f"seq/{what}"] = bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8)))
+    out["seq/algos:" + ",".join(sorted(a for a in algos if a))] = True
+    return out
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -91,7 +152,9 @@ def main():
                  # LL one-shot up to 1 MiB (larger buckets: the one-shot)
                  "ll": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
                  # the library defaults, fed a DDP-style bucket stream (vnode.DDP_STREAM)
-                 "ddp": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
+                 "ddp": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
+                 # tests/test_gpu_sequence_fuzz.py's random sequence at the defaults
+                 "seq": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
     direct_kw = {"direct": dict(direct_bytes=8 << 20, oneshot_bytes=-1, ll_bytes=-1),
                  "oneshot": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=-1),
                  "ll": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=1 << 20)}
@@ -106,8 +169,8 @@ def main():
         comm = C.init_communicator_rank(rank, world, dev, exchange,
                                         C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, lanes=lanes,
                                                      **direct_kw.get(mode, {})))
-        if mode == "ddp":
-            results.update(ddp_stream(comm, rank, world, orc, vnode))
+        if mode in ("ddp", "seq"):
+            results.update((ddp_stream if mode == "ddp" else seq_stream)(comm, rank, world, orc, vnode))
             dist.barrier()  # every rank's last kernel is done before any arena returns to the pool
             comm.destroy()
             continue
@@ -181,7 +244,7 @@ def main():
     allres = [None] * world
     dist.all_gather_object(allres, results)
     if rank == 0:
-        merged = {k: all(r[k] for r in allres) for k in results}
+        merged = {k: all(r.get(k, False) for r in allres) for k in results}
         print(json.dumps({"world": world, "fifo_modes": merged, "all_ok": all(merged.values())}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
