@@ -243,6 +243,38 @@ int comm_pool_count(unsigned generation) {
   return n;
 }
 
+bool GraphWorkPool::take(uint32_t n, uint32_t* start) {
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto it = free_ranges.begin(); it != free_ranges.end(); ++it)
+    if (it->second >= n) {
+      *start = it->first;
+      const uint32_t rest = it->second - n, at = it->first + n;
+      free_ranges.erase(it);
+      if (rest) free_ranges[at] = rest;
+      held += n;
+      return true;
+    }
+  return false;
+}
+
+void GraphWorkPool::give(uint32_t start, uint32_t n) {
+  std::lock_guard<std::mutex> lk(mu);
+  held -= n;
+  auto it = free_ranges.emplace(start, n).first;
+  auto next = std::next(it);
+  if (next != free_ranges.end() && it->first + it->second == next->first) {
+    it->second += next->second;
+    free_ranges.erase(next);
+  }
+  if (it != free_ranges.begin()) {
+    auto prev = std::prev(it);
+    if (prev->first + prev->second == it->first) {
+      prev->second += it->second;
+      free_ranges.erase(it);
+    }
+  }
+}
+
 // Live communicators' device structures -> their FIFO depth, so the external
 // launch (mccs_hip_launch_coll, whose reference-named kernels assume the
 // reference's 8 slots) can refuse a library communicator built with another.
@@ -358,7 +390,7 @@ mccsResult_t comm_alloc_local(Comm* c) {
     MCCS_HIP(rt().HostMallocMapped((void**)&c->h_graph_work, sizeof(mccsDevWork) * Comm::kGraphWorkEntries));
     MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_graph_work, c->h_graph_work));
     std::memset(c->h_graph_work, 0, sizeof(mccsDevWork) * Comm::kGraphWorkEntries);
-    c->graph_work_used = 0;
+    c->graph_pool = std::make_shared<GraphWorkPool>(Comm::kGraphWorkEntries);
   }
   {
     StepScope st("work done counters");

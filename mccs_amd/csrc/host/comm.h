@@ -13,6 +13,9 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -149,6 +152,24 @@ struct ChannelSchedule {  // plan.rs ChanWorkSchedule
   std::vector<int> work_func;                   // func id per work (for batching)
 };
 
+// Entries of a comm's graph work arena held by captured launches.  A
+// captured launch takes a contiguous range, which returns when the graph that
+// holds it is destroyed (rt().GraphOnDestroy), so graphs captured again and
+// again reuse the arena.  Shared with those callbacks, which may run on a
+// runtime thread after the comm is gone.
+struct GraphWorkPool {
+  std::mutex mu;
+  std::map<uint32_t, uint32_t> free_ranges;  // start -> entries
+  uint32_t held = 0;
+  explicit GraphWorkPool(uint32_t entries) { free_ranges[0] = entries; }
+  bool take(uint32_t n, uint32_t* start);  // first fit
+  void give(uint32_t start, uint32_t n);   // coalescing
+  uint32_t held_now() {
+    std::lock_guard<std::mutex> lk(mu);
+    return held;
+  }
+};
+
 struct Comm {
   int rank = 0, nranks = 1, device = 0;
   mccsCommConfig cfg{};
@@ -178,12 +199,12 @@ struct Comm {
   // Work lists of launches captured into HIP graphs: a graph replays the
   // same kernel arguments forever, so its works cannot live in the rolling
   // FIFO (slots get reused).  Captured launches take entries from this
-  // host-mapped arena for the comm's lifetime (allocated at init: allocation
-  // is not allowed while a stream captures).
+  // host-mapped arena (allocated at init: allocation is not allowed while a
+  // stream captures) until their graph is destroyed.
   static constexpr uint32_t kGraphWorkEntries = 2048;
   mccsDevWork* h_graph_work = nullptr;
   mccsDevWork* d_graph_work = nullptr;
-  uint32_t graph_work_used = 0;
+  std::shared_ptr<GraphWorkPool> graph_pool;
   uint32_t work_next = 0;      // work_queue_next_available
   uint32_t work_acked_min = 0; // work_queue_acked_min
   std::vector<uint32_t> chan_next;  // per channel work_queue_next_available

@@ -211,11 +211,24 @@ static bool eager_events() {
   return on;
 }
 
-// A launch being captured into a HIP graph: its works go to the comm's
-// graph arena, laid out like one FIFO upload (first work of channel i at
-// entry i, later ones chained by workNext relative to the head), with
-// inFifo = 0 so replays never write workFifoDone (common.h:153-155).
-static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld) {
+namespace {
+struct GraphWorkRelease {
+  std::shared_ptr<GraphWorkPool> pool;
+  uint32_t start, n;
+};
+void graph_work_release(void* p) {  // runs when the graph holding the range is gone
+  auto* r = (GraphWorkRelease*)p;
+  r->pool->give(r->start, r->n);
+  delete r;
+}
+}  // namespace
+
+// A launch being captured into HIP graph `graph`: its works go to a range of
+// the comm's graph arena, laid out like one FIFO upload (first work of channel
+// i at entry i, later ones chained by workNext relative to the head), with
+// inFifo = 0 so replays never write workFifoDone (common.h:153-155).  The
+// range returns to the arena when the graph and its executables are destroyed.
+static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld, hipGraph_t graph) {
   std::vector<int> chan_list;
   uint64_t mask = 0;
   uint32_t work_count = 0;
@@ -226,10 +239,17 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld) {
       work_count += (uint32_t)c->sched[ch].works.size();
     }
   if (chan_list.empty()) return mccsInternalError;
-  if (c->graph_work_used + work_count > Comm::kGraphWorkEntries)
-    MCCS_FAIL(mccsInvalidUsage, "graph work arena exhausted (%u of %u entries used)", c->graph_work_used,
-              Comm::kGraphWorkEntries);
-  mccsDevWork* head = c->h_graph_work + c->graph_work_used;
+  uint32_t start = 0;
+  if (!c->graph_pool->take(work_count, &start))
+    MCCS_FAIL(mccsInvalidUsage, "graph work arena exhausted (%u of %u entries held by live graphs, %u needed)",
+              c->graph_pool->held_now(), Comm::kGraphWorkEntries, work_count);
+  auto* rel = new GraphWorkRelease{c->graph_pool, start, work_count};
+  if (rt().GraphOnDestroy(graph, &graph_work_release, rel) != hipSuccess) {
+    MCCS_LOG("graph work entries %u..%u stay held for the comm's lifetime (no destroy callback)", start,
+             start + work_count - 1);
+    delete rel;
+  }
+  mccsDevWork* head = c->h_graph_work + start;
   const uint32_t nchan = (uint32_t)chan_list.size();
   uint32_t subsequent = nchan;
   for (uint32_t nth = 0; nth < nchan; ++nth) {
@@ -245,8 +265,7 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld) {
   std::atomic_thread_fence(std::memory_order_seq_cst);
   ld->mask = mask;
   ld->nch_used = (int)nchan;
-  ld->work = c->d_graph_work + c->graph_work_used;
-  c->graph_work_used += work_count;
+  ld->work = c->d_graph_work + start;
   ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
   ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
   for (auto& s : c->sched) s = ChannelSchedule{};
@@ -593,7 +612,9 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     // A capturing stream records this launch into a HIP graph: its work
     // list must outlive the FIFO's rolling slots (upload_work_graph).
     bool capturing = false;
+    hipGraph_t graph = nullptr;
     MCCS_HIP(rt().StreamIsCapturing(user_streams[idx[0]], &capturing));
+    if (capturing) MCCS_HIP(rt().CaptureGraph(user_streams[idx[0]], &graph));
     std::vector<LaunchDesc> lds(idx.size());
     mccsMultiLaunchArgs ma;
     mccsDirectArgs da;
@@ -618,7 +639,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
         for (size_t k = 0; k < idx.size(); ++k) MCCS_CHECK(upload_work_inline(comms[idx[k]], &lds[k], &ma));
       } else {
         for (size_t k = 0; k < idx.size(); ++k)
-          MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k]) : upload_work(comms[idx[k]], &lds[k]));
+          MCCS_CHECK(capturing ? upload_work_graph(comms[idx[k]], &lds[k], graph) : upload_work(comms[idx[k]], &lds[k]));
       }
       // Communicator launches carry their hand-off policy in the arguments
       // (one launch per device; blockIdx.y = rank slot when ranks share it).

@@ -16,6 +16,8 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <utility>
+#include <vector>
 
 #include "comm.h"
 
@@ -88,6 +90,19 @@ class HipRuntime final : public DeviceRuntime {
     hipError_t e = hipStreamIsCapturing(s, &st);
     *capturing = st == hipStreamCaptureStatusActive;
     return ret(e);
+  }
+  hipError_t CaptureGraph(hipStream_t s, hipGraph_t* g) override {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    *g = nullptr;
+    return ret(hipStreamGetCaptureInfo_v2(s, &st, nullptr, g, nullptr, nullptr));
+  }
+  hipError_t GraphOnDestroy(hipGraph_t g, void (*fn)(void*), void* arg) override {
+    hipUserObject_t obj = nullptr;
+    hipError_t e = hipUserObjectCreate(&obj, arg, fn, 1, hipUserObjectNoDestructorSync);
+    if (e != hipSuccess) return ret(e);
+    // the graph takes over the one reference; on failure the object (and so
+    // the callback) is left unreleased: what it guards stays held
+    return ret(hipGraphRetainUserObject(g, obj, 1, hipGraphUserObjectMove));
   }
   hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
     return ret(hipLaunchKernel(fn, grid, block, args, 0, s));
@@ -282,9 +297,43 @@ class FakeRuntime final : public DeviceRuntime {
          std::to_string((uintptr_t)e) + " event_dev=" + std::to_string(event_dev(e)));
     return hipSuccess;
   }
-  hipError_t StreamIsCapturing(hipStream_t, bool* capturing) override {
-    *capturing = false;
+  hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) override {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      *capturing = capture_.count(s) > 0;
+    }
     return inj("StreamIsCapturing");
+  }
+  hipError_t CaptureGraph(hipStream_t s, hipGraph_t* g) override {
+    if (hipError_t e = inj("CaptureGraph")) return e;
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = capture_.find(s);
+    if (it == capture_.end()) return hipErrorStreamCaptureUnmatched;
+    *g = (hipGraph_t)(uintptr_t)it->second;
+    return hipSuccess;
+  }
+  hipError_t GraphOnDestroy(hipGraph_t g, void (*fn)(void*), void* arg) override {
+    if (hipError_t e = inj("GraphOnDestroy")) return e;
+    std::lock_guard<std::mutex> lk(mu_);
+    on_destroy_[(int)(uintptr_t)g].emplace_back(fn, arg);
+    return hipSuccess;
+  }
+  // test hooks: a stream "captures" into graph id `graph` (0 ends it), and a
+  // "destroyed" graph runs the callbacks registered on it
+  void capture(hipStream_t s, int graph) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (graph > 0) capture_[s] = graph;
+    else capture_.erase(s);
+  }
+  int destroy_graph(int graph) {
+    std::vector<std::pair<void (*)(void*), void*>> fns;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fns.swap(on_destroy_[graph]);
+      on_destroy_.erase(graph);
+    }
+    for (auto& f : fns) f.first(f.second);
+    return (int)fns.size();
   }
   hipError_t LaunchKernelExt(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s,
                              hipEvent_t stop) override {
@@ -453,6 +502,8 @@ class FakeRuntime final : public DeviceRuntime {
   std::map<void*, int> ipc_open_;
   std::map<std::string, Fail> fail_;
   std::map<std::string, int> delay_ms_;
+  std::map<hipStream_t, int> capture_;
+  std::map<int, std::vector<std::pair<void (*)(void*), void*>>> on_destroy_;
   std::ostringstream log_, calls_;
 };
 
@@ -564,4 +615,25 @@ extern "C" int mccs_test_fake_delay(const char* call, int ms) {
   if (!f) return -1;
   f->delay(call, ms);
   return 0;
+}
+
+// Marks the fake stream `stream` (a handle value as the library's callers
+// pass it) as capturing into graph id `graph` (> 0), or ends its capture (0).
+extern "C" int mccs_test_fake_capture(void* stream, int graph) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  f->capture((hipStream_t)stream, graph);
+  return 0;
+}
+
+// "Destroys" fake graph `graph`: runs the callbacks registered on it (the HIP
+// user objects' destructors); returns how many ran, -1 without a fake.
+extern "C" int mccs_test_fake_destroy_graph(int graph) {
+  mccs::FakeRuntime* f;
+  {
+    std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+    f = mccs::g_fake.load();
+  }
+  return f ? f->destroy_graph(graph) : -1;
 }

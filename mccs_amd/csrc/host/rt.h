@@ -47,6 +47,12 @@ class DeviceRuntime {
   virtual hipError_t StreamSynchronize(hipStream_t s) = 0;
   virtual hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) = 0;
   virtual hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) = 0;
+  // The graph a capturing stream records into, and a host callback run once
+  // that graph and every executable graph instantiated from it are destroyed
+  // (a HIP user object the graph retains; the callback may run on a runtime
+  // thread and must make no HIP call).
+  virtual hipError_t CaptureGraph(hipStream_t s, hipGraph_t* g) = 0;
+  virtual hipError_t GraphOnDestroy(hipGraph_t g, void (*fn)(void*), void* arg) = 0;
   virtual hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) = 0;
   // The same launch with `stop` recorded by the dispatch's own completion
   // signal (hipExtLaunchKernel): no marker packet behind the kernel.

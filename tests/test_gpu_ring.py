@@ -502,6 +502,71 @@ def test_allreduce_captured_in_hip_graph(orc, n, count, bridge, fifo, monkeypatc
         vnode.destroy(comms)
 
 
+def test_graph_recapture_reuses_the_work_arena(orc, monkeypatch):
+    """A server that captures graphs again and again: 600 captures of a
+    grouped AllReduce whose works go through the graph work arena (more
+    entries than the arena's 2048), each graph destroyed after use, so its
+    entries return (a HIP user object the graph retains).  A graph captured
+    first and kept keeps its entries through all of them: torch destroys the
+    captured graph right after instantiation, so this also checks that the
+    executable graph holds the user object."""
+    import gc
+
+    import torch
+
+    monkeypatch.setenv("MCCS_INLINE_WORKS", "0")  # every captured launch takes arena entries
+    n, count = 2, 1 << 18
+    comms = C.init_all([0] * n, C.CommConfig(buffer_size=1 << 20, timeout_ms=10000))
+    try:
+        rng = np.random.default_rng(5)
+        s = torch.cuda.Stream()
+
+        def bufs():
+            return ([torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)],
+                    [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)])
+
+        def capture(send, recv):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                with C.group():
+                    for r in range(n):
+                        C.all_reduce(comms[r], send[r], recv[r], count, F16, 0, stream=s)
+            return g
+
+        def replay_and_check(g, send, recv):
+            inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
+            for r in range(n):
+                send[r].copy_(torch.from_numpy(inputs[r]).cuda())
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0], buff_size=1 << 20)
+            _check_all_equal([recv[r].cpu().numpy() for r in range(n)], exp, F16)
+
+        with C.group():  # warm-up outside capture
+            for r in range(n):
+                C.all_reduce(comms[r], *[b[r] for b in bufs()], count, F16, 0, stream=s)
+        s.synchronize()
+        kept_send, kept_recv = bufs()
+        kept = capture(kept_send, kept_recv)
+        replay_and_check(kept, kept_send, kept_recv)
+        send, recv = bufs()
+        per = C.task_schema(count * 2, comms[0].nchannels)[0]  # channels (= arena entries) per capture
+        assert 600 * per > 2048
+        for i in range(600):
+            g = capture(send, recv)
+            if i % 100 == 99:
+                replay_and_check(g, send, recv)
+            del g
+            gc.collect()
+        torch.cuda.synchronize()
+        replay_and_check(kept, kept_send, kept_recv)
+        del kept
+    finally:
+        torch.cuda.synchronize()
+        vnode.destroy(comms)
+
+
 @pytest.mark.parametrize("code,off", [(F16, 2), (F32, 4), (F32, 12), (BF16, 6)])
 def test_allreduce_misaligned_buffers(orc, code, off):
     """User buffers that are not 16-byte aligned take the typed element path
