@@ -126,7 +126,10 @@ typedef struct {
   int block_threads;    /* threads per workgroup (96..576, multiple of 32); 0 = MCCS_RING_MAX_THREADS (576) */
   int locality;         /* MCCS_LOCALITY_*; default RECEIVER (remote writes; SENDER = reference shm layout) */
   int fifo_memory;      /* MCCS_FIFO_*; default UNCACHED (MCCS_FIFO_MEMORY=uncached|release|device) */
-  int timeout_ms;       /* FIFO spin watchdog; 0 = 30000, < 0 = never */
+  int timeout_ms;       /* FIFO-wait watchdog: ms without progress before the kernel gives up (mccsTimeout);
+                           0 = 600000 (10 min, torch's default collective timeout: a peer may arrive
+                           minutes late, e.g. while rank 0 writes a checkpoint), < 0 = never;
+                           MCCS_TIMEOUT_MS overrides the default */
   int work_fifo_depth;  /* mccsDevWork slots (power of two); 0 = 4096 */
   int bridge_streams;   /* -1 (default): launch on the caller's stream; 1: user stream -> comm stream -> user stream events (libmccs two-stream bridge) */
   const int *rings;     /* channel_count x nranks send orders (comm_patterns_override); NULL = auto */

@@ -239,7 +239,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   // operator overrides (no rebuild needed): MCCS_LOCALITY=sender|receiver,
   // MCCS_LANES, MCCS_BLOCK_THREADS, MCCS_CHANNELS, MCCS_BUFFER_SIZE,
   // MCCS_BRIDGE_STREAMS, MCCS_FIFO_MEMORY=uncached|release|device,
-  // MCCS_FIFO_SLOTS, MCCS_DIRECT_BYTES, MCCS_ONESHOT_BYTES
+  // MCCS_FIFO_SLOTS, MCCS_DIRECT_BYTES, MCCS_ONESHOT_BYTES, MCCS_TIMEOUT_MS
   if (const char* v = std::getenv("MCCS_LOCALITY"))
     cfg->locality = (v[0] == 's' || v[0] == 'S') ? MCCS_LOCALITY_SENDER : MCCS_LOCALITY_RECEIVER;
   if (const char* v = std::getenv("MCCS_LANES")) cfg->lanes = std::atoi(v);
@@ -255,6 +255,7 @@ extern "C" void mccsCommConfigDefault(mccsCommConfig* cfg) {
   if (const char* v = std::getenv("MCCS_DIRECT_BYTES")) cfg->direct_bytes = std::atoi(v);
   if (const char* v = std::getenv("MCCS_ONESHOT_BYTES")) cfg->oneshot_bytes = std::atoi(v);
   if (const char* v = std::getenv("MCCS_LL_BYTES")) cfg->ll_bytes = std::atoi(v);
+  if (const char* v = std::getenv("MCCS_TIMEOUT_MS")) cfg->timeout_ms = std::atoi(v);
 }
 
 extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int* devices, const mccsCommConfig* cfg) {
@@ -585,7 +586,7 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
   if (err || abort_val) c->failed = true;
   if (err & MCCS_ERR_TIMEOUT)
     MCCS_FAIL(mccsTimeout, "rank %d: a FIFO wait passed the %d ms watchdog (error bits 0x%x)", c->rank,
-              c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms, err);
+              c->cfg.timeout_ms == 0 ? kDefaultTimeoutMs : c->cfg.timeout_ms, err);
   if (err || abort_val) MCCS_FAIL(mccsRemoteError, "rank %d: abortFlag %u, error bits 0x%x", c->rank, abort_val, err);
   return mccsSuccess;
 }

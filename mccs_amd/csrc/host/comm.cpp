@@ -122,7 +122,7 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
     k.fence_mode = MCCS_FENCE_UNCACHED_RELEASE;
   k.err_line = 1;  // d_abort is a 64-byte line of ours: errors go to its word 1
   k.fifo_slots = (uint32_t)c->cfg.fifo_slots;
-  const int tmo = c->cfg.timeout_ms == 0 ? 30000 : c->cfg.timeout_ms;
+  const int tmo = c->cfg.timeout_ms == 0 ? kDefaultTimeoutMs : c->cfg.timeout_ms;
   k.timeout_ticks = tmo < 0 ? 0 : (uint64_t)tmo * 100000ull;  // s_memrealtime: 100 MHz
   // one 4-step slice per chunk (2 slices in flight per lane): one flag
   // round trip and one drain per chunk instead of two; +6-27 % on the virtual

@@ -137,6 +137,11 @@ struct ConnectHandle {
   char pci[32];
 };
 constexpr uint32_t kHandleMagic = 0x6d636373;  // "mccs"
+// Default FIFO-wait watchdog (mccsCommConfig.timeout_ms = 0): 10 minutes,
+// torch's default collective timeout.  A rank may reach a collective minutes
+// before a peer (rank 0 writing a checkpoint while the others start the next
+// step); the watchdog counts time without progress, so it must outlast that.
+constexpr int kDefaultTimeoutMs = 600000;
 
 struct WorkElemHost {
   uint8_t nWarps;

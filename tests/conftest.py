@@ -4,6 +4,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# A hang in a test ends in 30 s, not the library's 10 min production default
+# (mccsCommConfig.timeout_ms); worker processes the tests start inherit it.
+os.environ.setdefault("MCCS_TIMEOUT_MS", "30000")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
