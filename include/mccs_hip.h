@@ -99,6 +99,14 @@ const void *mccs_hip_coll_kernel(int func, int dtype, int op);
 mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, struct mccsDevComm *comm, uint64_t channelMask,
                                   struct mccsDevWork *workHead, unsigned grid, unsigned block,
                                   hipStream_t stream);
+/* Watchdog of the reference-named kernels on the current device: ms without
+ * FIFO progress before a kernel raises abortFlag and returns; 0 = the default
+ * (10 min), < 0 = none.  The reference kernels have none and the reference host
+ * never reads abortFlag, so the default outlasts any late peer a deployment
+ * sees (a watchdog that fired on one would silently end every later collective
+ * of the communicator); tests lower it so a hang ends quickly.  Call it once
+ * per device before the launches it should govern. */
+mccsResult_t mccs_hip_set_ref_watchdog(int timeout_ms);
 
 typedef struct mccsComm *mccsComm_t;
 

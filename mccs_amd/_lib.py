@@ -94,6 +94,7 @@ SIGNATURES: dict[str, tuple] = {
     "mccs_hip_launch_coll": (
         _c_int, [_c_int, _c_int, _c_int, _c_void_p, ctypes.c_uint64, _c_void_p, ctypes.c_uint, ctypes.c_uint,
                  _c_void_p]),
+    "mccs_hip_set_ref_watchdog": (_c_int, [_c_int]),
     "mccsCommConfigDefault": (None, [_P(_CommConfig)]),
     "mccsCommConfigSize": (_c_size_t, []),
     "mccsCommConfigDefaultSized": (_c_int, [_P(_CommConfig), _c_size_t]),
@@ -142,7 +143,7 @@ SIGNATURES: dict[str, tuple] = {
 # Symbols appended after round 4: an older build (an A/B library under abvar/,
 # MCCS_LIB_PATH) loads without them; the in-tree build must export them
 # (tests/test_lib_exports.py).
-_ADDED_R5 = {"mccsGetLastErrorString", "mccsGetLastHipError"}
+_ADDED_R5 = {"mccsGetLastErrorString", "mccsGetLastHipError", "mccs_hip_set_ref_watchdog"}
 
 _lib = None
 

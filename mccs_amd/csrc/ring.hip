@@ -32,6 +32,11 @@ hipError_t ring_tu_ar_sum_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_tu_ar_prod_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_tu_ar_max_read_profile(unsigned long long* out, bool reset);
 hipError_t ring_tu_ar_min_read_profile(unsigned long long* out, bool reset);
+hipError_t ring_tu_ag_set_ref_watchdog(unsigned long long ticks);
+hipError_t ring_tu_ar_sum_set_ref_watchdog(unsigned long long ticks);
+hipError_t ring_tu_ar_prod_set_ref_watchdog(unsigned long long ticks);
+hipError_t ring_tu_ar_max_set_ref_watchdog(unsigned long long ticks);
+hipError_t ring_tu_ar_min_set_ref_watchdog(unsigned long long ticks);
 
 static const void* ar_kernel(int dtype, int op, bool multi) {
   if (dtype < 0 || dtype >= mccsNumTypes) return nullptr;
@@ -131,6 +136,23 @@ bool colocated_launch_running(int device, const mccsDevComm* comm) {
   return busy;
 }
 }  // namespace
+
+// The reference-named kernels' watchdog on the current device (every
+// translation unit holds its own copy): ms without FIFO progress before a
+// kernel raises abortFlag; 0 = the 10 min default, < 0 = none.
+extern "C" mccsResult_t mccs_hip_set_ref_watchdog(int timeout_ms) {
+  const unsigned long long ticks =
+      timeout_ms < 0 ? 0ull : (unsigned long long)(timeout_ms == 0 ? 600000 : timeout_ms) * 100000ull;
+  hipError_t (*const set[])(unsigned long long) = {
+      mccs::ring_tu_ag_set_ref_watchdog, mccs::ring_tu_ar_sum_set_ref_watchdog, mccs::ring_tu_ar_prod_set_ref_watchdog,
+      mccs::ring_tu_ar_max_set_ref_watchdog, mccs::ring_tu_ar_min_set_ref_watchdog};
+  for (auto f : set)
+    if (f(ticks) != hipSuccess) {
+      (void)hipGetLastError();
+      return mccsUnhandledCudaError;
+    }
+  return mccsSuccess;
+}
 
 extern "C" mccsResult_t mccs_hip_launch_coll(int func, int dtype, int op, mccsDevComm* comm, uint64_t channelMask,
                                              mccsDevWork* workHead, unsigned grid, unsigned block,

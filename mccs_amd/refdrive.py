@@ -42,6 +42,7 @@ release/acquire, 2-step slices, 8 FIFO slots, 30 s watchdog on abortFlag).
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 
 from . import _lib as L
@@ -254,7 +255,8 @@ class RefDrivenRank:
     default the reference ring on every channel."""
 
     def __init__(self, rank: int, n: int, device: int, allgather, nch: int = 2, rings=None,
-                 buff_size: int = 1 << 22, locality: str = "sender", fifo: str = "device"):
+                 buff_size: int = 1 << 22, locality: str = "sender", fifo: str = "device",
+                 watchdog_ms: int | None = None):
         if not 2 <= n or not 1 <= nch <= abi.MCCS_MAX_NCHANNELS or locality not in ("sender", "receiver") \
                 or fifo not in ("device", "host"):
             raise ValueError("bad reference-driven configuration")
@@ -266,6 +268,13 @@ class RefDrivenRank:
         self.lib = L.load()
         h = hip()
         _ok(h.hipSetDevice(device), "hipSetDevice")
+        # the reference kernels' watchdog on this device: 10 min unless the
+        # caller (or MCCS_TIMEOUT_MS) sets one -- the tests and the bench bound
+        # a hang to seconds
+        if watchdog_ms is None and os.environ.get("MCCS_TIMEOUT_MS"):
+            watchdog_ms = int(os.environ["MCCS_TIMEOUT_MS"])
+        if watchdog_ms is not None:
+            L.check(self.lib.mccs_hip_set_ref_watchdog(int(watchdog_ms)), "mccs_hip_set_ref_watchdog")
         self._dev_allocs, self._host_allocs, self._opened, self._segs = [], [], [], []
         # -- connector memory: [SendBufMeta][RecvBufMeta][FIFO] per channel, one allocation
         self.stride = 2 * META + buff_size
@@ -583,7 +592,8 @@ ROTATE_BYTES = 1152 << 20
 
 
 def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbytes: int, variants: list[dict],
-                          warmup: int = 3, steps: int = 10, group=None, rotate_bytes: int = ROTATE_BYTES) -> list[dict]:
+                          warmup: int = 3, steps: int = 10, group=None, rotate_bytes: int = ROTATE_BYTES,
+                          watchdog_ms: int | None = None) -> list[dict]:
     """Times every variant at `nbytes` fp32 per rank (algbw = nbytes / t per
     AllReduce, max over ranks), each gated by an exact-sum check on every
     rank.  Step i uses send/recv pair i mod P, P = ceil(rotate_bytes /
@@ -627,7 +637,7 @@ def time_reference_driven(torch, dist, rank: int, world: int, device: int, nbyte
         rr, err = None, None
         try:
             rr = RefDrivenRank(rank, world, device, allgather, nch=v["nch"], rings=v["rings"],
-                               locality=v["locality"], fifo=v.get("fifo", "device"))
+                               locality=v["locality"], fifo=v.get("fifo", "device"), watchdog_ms=watchdog_ms)
         except Exception as e:  # noqa: BLE001
             err = f"setup: {type(e).__name__}: {e}"[:300]
         if agree(err is None):

@@ -899,8 +899,10 @@ def reference_driven_leg(torch, dist, rank, world, device, nbytes) -> dict:
     share = torch.cuda.device_count() < world
     max_ch = max(2, 128 // world) if share else 32
     try:
+        # a hang on a bad node ends in 20 s, not the kernels' 10 min default
         rows = refdrive.time_reference_driven(torch, dist, rank, world, device, nbytes,
-                                              refdrive.default_variants(world, C.default_rings, max_ch))
+                                              refdrive.default_variants(world, C.default_rings, max_ch),
+                                              watchdog_ms=20000)
     except Exception as e:  # noqa: BLE001
         rows = [{"error": f"{type(e).__name__}: {e}"[:300]}]
     torch.cuda.empty_cache()

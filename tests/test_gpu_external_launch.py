@@ -32,6 +32,47 @@ def _works(nch, send, recv, count, nthr):
     return works
 
 
+@pytest.fixture(autouse=True)
+def _ref_watchdog():
+    """The reference-named kernels' watchdog defaults to 10 min (no late
+    peer may trip it in a deployment); a hang here should end in 30 s."""
+    lib = _lib.load()
+    assert lib.mccs_hip_set_ref_watchdog(30000) == 0
+    yield
+    lib.mccs_hip_set_ref_watchdog(30000)
+
+
+def test_ref_watchdog_is_settable():
+    """mccs_hip_set_ref_watchdog governs the reference-named kernels: a rank
+    launched without its peer gives up after the set 300 ms (abortFlag
+    raised, the kernel ends), and 0 restores the 10 min default."""
+    import torch
+
+    lib = _lib.load()
+    comms = C.init_all([0, 0], C.CommConfig(lanes=1, fifo_slots=8))
+    try:
+        nch, nthr, count = comms[0].nchannels, 544, 1 << 16
+        x, y = torch.ones(count, device="cuda"), torch.zeros(count, device="cuda")
+        wb = torch.frombuffer(bytearray(bytes(_works(nch, x.data_ptr(), y.data_ptr(), count, nthr))),
+                              dtype=torch.uint8).cuda()
+        torch.cuda.synchronize()
+        assert lib.mccs_hip_set_ref_watchdog(300) == 0
+        st = torch.cuda.Stream()
+        t0 = time.perf_counter()
+        assert lib.mccs_hip_launch_coll(FUNC_ALLREDUCE, F32, 0, comms[0].dev_comm(), (1 << nch) - 1, wb.data_ptr(),
+                                        nch, nthr, st.cuda_stream) == 0
+        st.synchronize()  # no peer ever runs: only the watchdog ends it
+        waited = time.perf_counter() - t0
+        assert 0.25 < waited < 10, waited
+        with pytest.raises(_lib.MccsError, match="abortFlag 1"):
+            comms[0].sync()
+        assert lib.mccs_hip_set_ref_watchdog(0) == 0 and lib.mccs_hip_set_ref_watchdog(-1) == 0
+    finally:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.destroy()
+
+
 def test_colocated_external_launch_refused_while_peer_runs():
     import torch
 
