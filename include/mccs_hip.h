@@ -208,11 +208,13 @@ mccsResult_t mccsGroupEnd(void);
 mccsResult_t mccsCommSync(mccsComm_t comm);
 /* Raises the comm's abortFlag: in-flight kernels exit at their next poll. */
 mccsResult_t mccsCommAbort(mccsComm_t comm);
-/* Frees the comm.  Across processes, destroy only after every rank's last
- * collective has completed (mccsCommSync on every rank, then an out-of-band
- * barrier): a peer's last flag post can land in this rank's FIFO arena after
- * this rank's own kernel finished, and the arena goes back to a per-process
- * pool that the next communicator of the same size reuses. */
+/* Frees the comm after its last launch completed; no barrier with the peers
+ * is needed.  A peer's kernel may still post into this rank's FIFO arena after
+ * this rank's own kernel finished, so the arena goes back to a per-process pool
+ * but is handed to a new communicator only once every peer has destroyed its
+ * side too (each peer's destroy writes a release word into the arena, after
+ * its own kernels ended).  A peer that never destroys (a crashed process)
+ * leaves the arena pooled and unused. */
 mccsResult_t mccsCommDestroy(mccsComm_t comm);
 /* rank, nranks, device, channels, lanes, block threads, fifo memory kind
  * (MCCS_FIFO_*: the hand-off mode the comm's launches run). */

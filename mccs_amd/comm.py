@@ -188,9 +188,9 @@ class Communicator:
         _lib.check(_sig().mccsCommAbort(self._h), "mccsCommAbort")
 
     def destroy(self) -> None:
-        """mccsCommDestroy.  Across processes, call it only after every rank's
-        last collective completed (sync on every rank, then a barrier): a
-        peer's last flag post can still land in this rank's pooled FIFO arena."""
+        """mccsCommDestroy: frees the comm once its last launch completed.  No
+        barrier with the peers is needed: the FIFO arena is reused only after
+        every peer destroyed its side (include/mccs_hip.h)."""
         if self._h.value:
             _lib.check(_sig().mccsCommDestroy(self._h), "mccsCommDestroy")
             self._h = ctypes.c_void_p(0)

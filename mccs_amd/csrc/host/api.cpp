@@ -292,6 +292,11 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
   }
   for (int i = 0; i < nranks && r == mccsSuccess; ++i)
     for (int j = 0; j < nranks && r == mccsSuccess; ++j) r = enable_peer(devices[i], devices[j]);
+  if (r == mccsSuccess)  // every rank's arena is every peer's to write (released at comm_free)
+    for (int i = 0; i < nranks; ++i) {
+      cs[i]->arena_shared = nranks > 1;
+      for (int j = 0; j < nranks; ++j) cs[i]->peer_epoch[j] = j == i ? 0 : cs[j]->arena_epoch;
+    }
   if (r == mccsSuccess) {
     bool all_uc = true, release = false;
     for (int i = 0; i < nranks; ++i) {
@@ -371,6 +376,8 @@ extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks,
     delete c;
     return r;
   }
+  c->arena_shared = nranks > 1;  // exported: any peer may map it from now on
+  h.arena_epoch = c->arena_epoch;
   h.magic = kHandleMagic;
   h.rank = rank;
   h.nranks = nranks;
@@ -497,6 +504,7 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
     MCCS_HIP(rt().IpcOpenMemHandle(&p, h.ipc));
     c->peer_arena[r] = (char*)p;
     c->peer_opened_ipc[r] = true;
+    c->peer_epoch[r] = h.arena_epoch;
   }
   c->all_uncached = all_uc;
   c->fifo_release = release;

@@ -144,12 +144,23 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
 // communicators of nearby shapes share arenas and a process that creates many
 // shapes does not keep one arena per shape (a 2,000-case fuzz on one GPU ran
 // out of HBM at case 876 with exact-size pooling).
+//
+// An arena is handed out again only once every peer of its last communicator
+// has released it: a peer's kernel may still post head lines into it after
+// this rank's own kernel finished, and such a late post would land in the next
+// tenant's flags.  Each peer writes the tenancy's epoch into the arena's
+// release word for its rank when it destroys its communicator (comm_free,
+// after its last kernel ended); until every awaited word holds the epoch the
+// arena stays pooled but unused.
 struct PooledArena {
   unsigned generation;  // rt_generation() of the runtime that allocated it
   int device;
   bool uncached;
   size_t bytes;
   char* ptr;
+  uint64_t epoch;        // the last tenancy
+  size_t release_off;    // its release words (ArenaLayout::release_off of that tenancy)
+  uint64_t waiting;      // bit r: rank r's release not seen yet
 };
 static std::mutex g_pool_mu;
 static std::vector<PooledArena> g_pool;
@@ -163,13 +174,24 @@ static size_t arena_class(size_t need) {
   return (need + g - 1) / g * g;
 }
 
+// Clears the bits of the peers whose release word now holds the epoch
+// (g_pool_mu held).  True when nothing is awaited.
+static bool pool_released(PooledArena& a) {
+  if (!a.waiting) return true;
+  uint64_t w[ArenaLayout::kReleaseBytes / sizeof(uint64_t)];
+  if (rt().Memcpy(w, a.ptr + a.release_off, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) return false;
+  for (int r = 0; r < 64; ++r)
+    if ((a.waiting >> r & 1) && w[r] == a.epoch) a.waiting &= ~(1ull << r);
+  return a.waiting == 0;
+}
+
 static char* pool_take(int device, bool uncached, size_t need, size_t* got) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
   size_t best = g_pool.size();
   for (size_t i = 0; i < g_pool.size(); ++i) {
-    const PooledArena& a = g_pool[i];
+    PooledArena& a = g_pool[i];
     if (a.generation == rt_generation() && a.device == device && a.uncached == uncached && a.bytes >= need &&
-        a.bytes <= 2 * need && (best == g_pool.size() || a.bytes < g_pool[best].bytes))
+        a.bytes <= 2 * need && (best == g_pool.size() || a.bytes < g_pool[best].bytes) && pool_released(a))
       best = i;
   }
   if (best == g_pool.size()) return nullptr;
@@ -179,23 +201,26 @@ static char* pool_take(int device, bool uncached, size_t need, size_t* got) {
   return p;
 }
 
-static void pool_give(int device, bool uncached, size_t bytes, char* p) {
+static void pool_give(int device, bool uncached, size_t bytes, char* p, uint64_t epoch = 0, size_t release_off = 0,
+                      uint64_t waiting = 0) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.push_back(PooledArena{rt_generation(), device, uncached, bytes, p});
+  g_pool.push_back(PooledArena{rt_generation(), device, uncached, bytes, p, epoch, release_off, waiting});
 }
 
-// Out of device memory: return this device's pooled uncached arenas to the
-// runtime (no live communicator uses them).  Only uncached ones: whatever
-// re-allocates such a range at worst sees uncached behaviour, which is still
-// correct; a freed coarse range re-allocated as an uncached arena is the case
-// the pool exists to avoid.  Returns the bytes released.
+// Out of device memory: return this device's released pooled uncached arenas
+// to the runtime (no communicator uses them and no peer will write them).
+// Only uncached ones: whatever re-allocates such a range at worst sees
+// uncached behaviour, which is still correct; a freed coarse range
+// re-allocated as an uncached arena is the case the pool exists to avoid.
+// Returns the bytes released.
 static size_t pool_release_uncached(int device) {
   std::vector<char*> drop;
   size_t bytes = 0;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     for (size_t i = 0; i < g_pool.size();)
-      if (g_pool[i].generation == rt_generation() && g_pool[i].device == device && g_pool[i].uncached) {
+      if (g_pool[i].generation == rt_generation() && g_pool[i].device == device && g_pool[i].uncached &&
+          pool_released(g_pool[i])) {
         drop.push_back(g_pool[i].ptr);
         bytes += g_pool[i].bytes;
         g_pool.erase(g_pool.begin() + i);
@@ -227,6 +252,12 @@ static hipError_t arena_alloc(int device, bool uncached, size_t need, char** p, 
   return hipSuccess;
 }
 
+// A tenancy id unique in this process and across processes: pid, then a count.
+static uint64_t next_arena_epoch() {
+  static std::atomic<uint32_t> n{0};
+  return ((uint64_t)(uint32_t)getpid() << 32) | (uint64_t)(n.fetch_add(1) + 1);
+}
+
 // A fake runtime's "device" memory dies with it (rt.cpp): its pooled arenas
 // must never be handed out again.  Real HIP arenas (generation 0) stay.
 void comm_pool_drop_generation(unsigned generation) {
@@ -240,6 +271,13 @@ int comm_pool_count(unsigned generation) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
   int n = 0;
   for (const auto& a : g_pool) n += a.generation == generation;
+  return n;
+}
+
+int comm_pool_waiting(unsigned generation) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  int n = 0;
+  for (auto& a : g_pool) n += a.generation == generation && !pool_released(a);
   return n;
 }
 
@@ -294,6 +332,7 @@ mccsResult_t comm_switch_to_device_arena(Comm* c) {
   StepScope st("device arena fallback");
   DeviceGuard g(c->device);
   const size_t bytes = c->layout.total();
+  // (its export was refused, so no peer ever saw it: nothing to await)
   if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->own_arena_bytes, c->own_arena);
   c->own_arena = nullptr;
   c->own_arena_uncached = false;
@@ -359,6 +398,9 @@ mccsResult_t comm_alloc_local(Comm* c) {
       MCCS_LOG("rank %d arena %p bytes %zu uncached=%d", c->rank, (void*)c->own_arena, bytes,
                (int)c->own_arena_uncached);
     c->peer_arena[c->rank] = c->own_arena;
+    c->arena_epoch = next_arena_epoch();
+    c->arena_shared = false;
+    c->peer_epoch.assign(c->nranks, 0);
   }
   {
     StepScope st("FIFO arena zero-fill");
@@ -547,9 +589,26 @@ mccsResult_t comm_free(Comm* c) {
   }
   while (c->waiters.load() > 0) sched_yield();  // a fused comm's wait on our event
   if (c->stream) (void)rt().StreamSynchronize(c->stream);
+  // Our kernels are done: release every peer's arena (its release word for
+  // our rank gets its tenancy's epoch), then unmap it.  Best effort: a peer
+  // arena whose release is lost stays pooled, unused, in the peer's process.
+  for (int r = 0; r < (int)c->peer_arena.size(); ++r) {
+    if (r == c->rank || !c->peer_arena[r] || r >= (int)c->peer_epoch.size() || !c->peer_epoch[r]) continue;
+    const uint64_t ep = c->peer_epoch[r];
+    if (rt().Memcpy(c->peer_arena[r] + c->layout.release_off() + sizeof(uint64_t) * c->rank, &ep, sizeof(ep),
+                    hipMemcpyHostToDevice) != hipSuccess)
+      MCCS_LOG("rank %d: could not release rank %d's FIFO arena", c->rank, r);
+  }
   for (int r = 0; r < (int)c->peer_arena.size(); ++r)
     if (c->peer_opened_ipc[r] && c->peer_arena[r]) (void)rt().IpcCloseMemHandle(c->peer_arena[r]);
-  if (c->own_arena) pool_give(c->device, c->own_arena_uncached, c->own_arena_bytes, c->own_arena);
+  if (c->own_arena) {
+    uint64_t waiting = 0;
+    if (c->arena_shared)
+      for (int r = 0; r < c->nranks; ++r)
+        if (r != c->rank) waiting |= 1ull << r;
+    pool_give(c->device, c->own_arena_uncached, c->own_arena_bytes, c->own_arena, c->arena_epoch,
+              c->layout.release_off(), waiting);
+  }
   for (auto p : c->d_peers)
     if (p) (void)rt().Free(p);
   for (auto p : c->d_user_ranks)

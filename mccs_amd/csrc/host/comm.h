@@ -97,9 +97,13 @@ struct ArenaLayout {
   size_t oneshot_slot = 0;  // bytes of one one-shot slot
   size_t ll_slot = 0;       // bytes of one LL one-shot slot (2 x the LL bucket bytes)
   static constexpr size_t kLinesBytes = (size_t)MCCS_MAX_LANES * MCCS_FLAG_LINE_BYTES;  // 8 KiB
+  // after the flag lines: one release word per rank (kMaxRanks), written by
+  // that peer when it destroys its communicator (comm_free)
+  static constexpr size_t kReleaseBytes = 64 * sizeof(uint64_t);
   size_t head_off(int c) const { return (size_t)c * 2 * kLinesBytes; }
   size_t tail_off(int c) const { return (size_t)c * 2 * kLinesBytes + kLinesBytes; }
-  size_t flags_bytes() const { return (((size_t)nch * 2 * kLinesBytes) + 65535) & ~(size_t)65535; }
+  size_t release_off() const { return (size_t)nch * 2 * kLinesBytes; }
+  size_t flags_bytes() const { return (release_off() + kReleaseBytes + 65535) & ~(size_t)65535; }
   size_t data_off(int c) const { return flags_bytes() + (size_t)c * fifo_bytes; }
   size_t ring_total() const { return flags_bytes() + (size_t)nch * fifo_bytes; }
   size_t direct_off() const { return (ring_total() + 65535) & ~(size_t)65535; }
@@ -135,6 +139,9 @@ struct ConnectHandle {
   // PCI bus id of the rank's GPU: device ordinals are local to a process
   // (HIP_VISIBLE_DEVICES), so co-location and peer lookups use this
   char pci[32];
+  // this communicator's tenancy of the rank's FIFO arena: peers write it into
+  // the arena's release word when they destroy their communicator
+  uint64_t arena_epoch;
 };
 constexpr uint32_t kHandleMagic = 0x6d636373;  // "mccs"
 // Default FIFO-wait watchdog (mccsCommConfig.timeout_ms = 0): 10 minutes,
@@ -185,6 +192,13 @@ struct Comm {
   char* own_arena = nullptr;
   size_t own_arena_bytes = 0;  // the allocation (its size class), >= layout.total()
   bool own_arena_uncached = true;
+  // Release protocol of the pooled arenas: this comm's tenancy of its own
+  // arena (unique per process and comm), whether peers may hold or have held
+  // it (exported / built into their device structures), and each peer's
+  // tenancy, written back into that peer's arena at comm_free.
+  uint64_t arena_epoch = 0;
+  bool arena_shared = false;
+  std::vector<uint64_t> peer_epoch;
   std::vector<char*> peer_arena;
   std::vector<bool> peer_opened_ipc;
   bool all_uncached = true;
@@ -283,7 +297,8 @@ mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream
 mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one
 int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live library comm's device struct, else 0
 void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
-int comm_pool_count(unsigned generation);             // arenas pooled under that runtime (tests)
+int comm_pool_count(unsigned generation);
+int comm_pool_waiting(unsigned generation);  // pooled arenas still awaiting a peer's release (tests)             // arenas pooled under that runtime (tests)
 // gate.cpp
 bool gate_wanted(bool distinct_gpus);
 int gate_env();  // MCCS_GATE: -1 unset, else its value

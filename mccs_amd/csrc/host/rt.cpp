@@ -637,3 +637,7 @@ extern "C" int mccs_test_fake_destroy_graph(int graph) {
   }
   return f ? f->destroy_graph(graph) : -1;
 }
+
+// Pooled FIFO arenas of the current runtime still awaiting a peer's release
+// (comm.cpp pool; tests of the release protocol).
+extern "C" int mccs_test_pool_waiting(void) { return mccs::comm_pool_waiting(mccs::rt_generation()); }

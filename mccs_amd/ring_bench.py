@@ -555,8 +555,7 @@ def direct_sweep(torch, dist, C, rank, world, device, dev, exchange, config, rin
     try:
         torch.cuda.synchronize()
     finally:
-        # every rank's last kernel is done before any arena returns to the pool
-        # (mccsCommDestroy contract, include/mccs_hip.h)
+        # every rank's last kernel is done before the timing's next step
         dist.barrier()
         for cm in comms.values():
             try:

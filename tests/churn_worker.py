@@ -7,8 +7,9 @@
 Every cycle: one rank per process connects a communicator of a shape drawn
 from the same seed on every rank (IPC export / open of every peer's arena),
 runs the int32 known-answer AllReduce on the ring and on the default
-small-bucket kernel, then all ranks meet at a barrier and destroy it (the
-destroy contract, include/mccs_hip.h).  Rank 0 prints one JSON line: every
+small-bucket kernel, then destroys it -- after a barrier with the peers, or
+(CHURN_NO_BARRIER=1) right away: the library itself holds a destroyed rank's
+arena back until every peer destroyed its side.  Rank 0 prints one JSON line: every
 cycle exact, and the largest drop of any rank's free GPU memory from the
 end of the first round of shapes (the arena pool warm) to the last cycle.
 """
@@ -39,6 +40,7 @@ def main():
         dist.all_gather_object(out, b)
         return out
 
+    no_barrier = os.environ.get("CHURN_NO_BARRIER") == "1"
     ok, free = [], []
     shapes = churn_shapes(11, SHAPES, [world])
     for i, (_, cfg) in enumerate(shapes):
@@ -53,7 +55,8 @@ def main():
         ok.append(good)
         del send, recv
         torch.cuda.synchronize()
-        dist.barrier()  # every rank's last kernel is done before any arena returns to the pool
+        if not no_barrier:
+            dist.barrier()
         comm.destroy()
         torch.cuda.empty_cache()
         if i in (SHAPES - 1, len(shapes) - 1):

@@ -24,6 +24,7 @@ def lib(monkeypatch):
     monkeypatch.setenv("MCCS_TEST_HOOKS", "1")
     monkeypatch.setenv("MCCS_GATE", "0")
     lib.mccs_test_fake_fail.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    lib.mccs_test_pool_waiting.restype = ctypes.c_int
     assert lib.mccs_test_fake_runtime(0) == 0
     assert lib.mccs_test_fake_runtime(2) == 0
     yield lib
@@ -96,3 +97,30 @@ def test_out_of_memory_releases_pooled_uncached_arenas(lib):
     for c in comms:
         c.destroy()
     assert _pooled(lib) == 3
+
+
+def test_arena_waits_for_every_peer_release(lib):
+    """A peer's kernel may post into this rank's arena after this rank's own
+    kernel ended, so a destroyed communicator's arena is reused only after
+    every peer destroyed its side (each writes the tenancy's epoch into the
+    arena's release word for its rank).  Until then a new communicator gets a
+    fresh arena -- the destroy contract no longer rests on the caller."""
+    from test_rank_per_process import _connect_per_process
+
+    comms, _ = _connect_per_process(lib, 2)  # one rank per "process", devices 0 and 1
+    comms[0].destroy()
+    assert lib.mccs_test_pool_waiting() == 1  # rank 0's arena: rank 1 may still post into it
+    _calls(lib)
+    fresh = C.init_all([0, 1])
+    assert _calls(lib).count("MallocUncached") == 2, "rank 0's unreleased arena was handed out again"
+    for c in fresh:
+        c.destroy()  # in-process ranks release each other
+    assert lib.mccs_test_pool_waiting() == 1
+    comms[1].destroy()  # rank 1 releases rank 0's arena (rank 0 released rank 1's at its own destroy)
+    assert lib.mccs_test_pool_waiting() == 0
+    _calls(lib)
+    again = [C.init_all([0, 1]) for _ in range(2)]
+    assert _calls(lib).count("MallocUncached") == 0  # all four pooled arenas are free again
+    for cs in again:
+        for c in cs:
+            c.destroy()

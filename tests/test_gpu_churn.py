@@ -89,11 +89,17 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_process_churn_keeps_memory_flat(world):
+@pytest.mark.parametrize("world,no_barrier", [(2, False), (4, False), (2, True), (4, True)])
+def test_process_churn_keeps_memory_flat(world, no_barrier):
+    """no_barrier: every rank destroys its communicator as soon as its own
+    collectives are done, with no barrier among the ranks (the arena release
+    protocol, comm.cpp pool, keeps a destroyed arena from a new tenant until
+    every peer destroyed its side); the next cycle's communicators may then
+    need fresh arenas while the old ones wait, so memory may grow by a few
+    arenas, never by one per cycle."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(HERE, "churn_worker.py")]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CHURN_NO_BARRIER="1" if no_barrier else "0")
     for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES", "MCCS_LL_BYTES"):
         env.pop(k, None)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=os.path.dirname(HERE))
@@ -103,4 +109,4 @@ def test_process_churn_keeps_memory_flat(world):
     res = json.loads(lines[-1])
     print(f"process churn, {world} processes:", res)
     assert res["all_ok"], res
-    assert res["max_drift_bytes"] < DRIFT_BYTES, res
+    assert res["max_drift_bytes"] < (4 if no_barrier else 1) * DRIFT_BYTES, res
