@@ -290,15 +290,15 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   // workgroup on the same bytes in phases 1 and 3.
   const bool self_wait = a.mode == MCCS_DIRECT_ONE_SHOT && me.send == me.recv;
   MCCS_DTRACE(kDtStart);
-  // Prologue: lanes of wave 0 load the state words (and the abort flag) in
-  // one round trip.
+  // Prologue: lanes of wave 0 load the state words in one round trip.  The
+  // abort flag is not read here: it is host memory (comm.cpp
+  // place_abort_line), and a read from every workgroup at once cost 1.2 us at
+  // 32 KiB and 22 us at 512 KiB per call; the waits below check it.
   if (threadIdx.x < 64) {
     const uint32_t lane = threadIdx.x;
     uint64_t v = 0;
     if (lane < MCCS_DIRECT_ST_WORDS)
       v = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_STATE) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else if (lane == MCCS_DIRECT_ST_WORDS)
-      v = abort_raised(abortFlag) ? 1 : 0;
     if (lane == MCCS_DIRECT_ST_LAUNCHES) sh.seq = v + 1;
     if (lane == MCCS_DIRECT_ST_E_IN) sh.e_in = v;
     if (lane >= 2 && lane < 2 + MCCS_DIRECT_MAX_RANKS) sh.e_out[lane - 2] = v;
@@ -586,7 +586,7 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
   if (threadIdx.x == 0) {
     s_seq = __hip_atomic_load((uint64_t*)(mine + MCCS_DIRECT_STATE) + MCCS_DIRECT_ST_LAUNCHES, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT) + 1;
-    s_ok = !abort_raised(abortFlag);
+    s_ok = 1;  // abortFlag (host memory) is checked in the wait, not here: see the two-shot prologue
   }
   if (threadIdx.x < 64) ((uint32_t*)s_idx2rank)[threadIdx.x] = ((const uint32_t*)a.idx2rank)[threadIdx.x];
   __syncthreads();

@@ -588,9 +588,8 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
   // the communicator's abort line: word 0 abortFlag, word 1 the error bits its
   // kernels reported (ring_cfg.h), so another communicator's failure never
   // shows up here
-  uint32_t line[2] = {0, 0};
-  MCCS_HIP(rt().Memcpy(line, c->d_abort, sizeof(line), hipMemcpyDeviceToHost));
-  const uint32_t abort_val = line[0], err = line[1];
+  const uint32_t abort_val = __atomic_load_n(c->h_abort, __ATOMIC_ACQUIRE);
+  const uint32_t err = __atomic_load_n(c->h_abort + 1, __ATOMIC_ACQUIRE);
   if (err || abort_val) c->failed = true;
   if (err & MCCS_ERR_TIMEOUT)
     MCCS_FAIL(mccsTimeout, "rank %d: a FIFO wait passed the %d ms watchdog (error bits 0x%x)", c->rank,
@@ -602,10 +601,10 @@ extern "C" mccsResult_t mccsCommSync(mccsComm_t comm) {
 extern "C" mccsResult_t mccsCommAbort(mccsComm_t comm) {
   Comm* c = (Comm*)comm;
   if (!c) return mccsInvalidArgument;
-  DeviceGuard g(c->device);
-  const uint32_t one = 1;
-  MCCS_HIP(rt().Memcpy(c->d_abort, &one, sizeof(one), hipMemcpyHostToDevice));
   c->failed = true;
+  // a CPU store into the host-mapped line: no stream, so nothing can queue it
+  // behind the kernel it must stop (comm.cpp place_abort_line)
+  if (c->h_abort) __atomic_store_n(c->h_abort, 1u, __ATOMIC_SEQ_CST);
   return mccsSuccess;
 }
 

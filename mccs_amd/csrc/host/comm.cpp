@@ -326,6 +326,26 @@ int comm_fifo_slots_of(const void* d_comm) {
   return it == g_live_fifo_slots.end() ? 0 : it->second;
 }
 
+// The abort line must reach a kernel that polls it right after the host writes
+// it (mccsCommAbort, the node gate's reset), with no GPU queue in between: a
+// copy on any stream can wait behind the very kernel it must stop, since HIP
+// maps a process's streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4
+// here) and a stream created for the abort can share the spinning kernel's
+// queue -- on MI355X an abort written that way was seen only when the kernel's
+// 30 s watchdog ended it.  (A line in coarse device memory could also be held
+// stale by L2, which a host DMA write does not update.)  So the line is
+// host-mapped memory the CPU writes and reads directly; kernels read it over
+// PCIe only when they check (every 64 polls of a wait, and between works).
+// (The reference leaves its abortFlag uninitialised, device.rs:157; here it
+// starts at zero.)
+mccsResult_t place_abort_line(Comm* c) {
+  StepScope st("abort line");
+  MCCS_HIP(rt().HostMallocMapped((void**)&c->h_abort, 64));
+  std::memset(c->h_abort, 0, 64);
+  MCCS_HIP(rt().HostGetDevicePointer((void**)&c->d_abort, c->h_abort));
+  return mccsSuccess;
+}
+
 // Swap this comm's uncached arena for a plain device arena (used when IPC
 // export of the uncached one is refused).  The old range goes back to the pool.
 mccsResult_t comm_switch_to_device_arena(Comm* c) {
@@ -408,10 +428,9 @@ mccsResult_t comm_alloc_local(Comm* c) {
     MCCS_HIP(rt().FlushCaches());
     MCCS_HIP(rt().DeviceSynchronize());
   }
+  MCCS_CHECK(place_abort_line(c));
   {
     StepScope st("device comm");
-    MCCS_HIP(rt().Malloc((void**)&c->d_abort, 64));
-    MCCS_HIP(rt().Memset(c->d_abort, 0, 64));  // the reference leaves it uninitialised (device.rs:157)
     MCCS_HIP(rt().Malloc((void**)&c->d_comm,
                          sizeof(mccsDevCommAndChannels) + sizeof(mccsRingConnView) * MCCS_MAX_NCHANNELS));
     c->d_view = (mccsRingConnView*)((char*)c->d_comm + sizeof(mccsDevCommAndChannels));
@@ -614,7 +633,7 @@ mccsResult_t comm_free(Comm* c) {
   for (auto p : c->d_user_ranks)
     if (p) (void)rt().Free(p);
   if (c->d_comm) (void)rt().Free(c->d_comm);
-  if (c->d_abort) (void)rt().Free(c->d_abort);
+  if (c->h_abort) (void)rt().HostFree(c->h_abort);
   if (c->h_work) (void)rt().HostFree(c->h_work);
   if (c->h_graph_work) (void)rt().HostFree(c->h_graph_work);
   if (c->h_done) (void)rt().HostFree(c->h_done);

@@ -208,7 +208,11 @@ struct Comm {
   std::vector<mccsDevChannelPeer*> d_peers;
   std::vector<int*> d_user_ranks;
   mccsRingConnView* d_view = nullptr;  // per channel, in d_comm's allocation after the channels
+  // The abort line (word 0 abortFlag, word 1 error bits) in host-mapped memory:
+  // the host reads and writes it with plain CPU accesses (comm.cpp
+  // place_abort_line), kernels through d_abort.
   uint32_t* d_abort = nullptr;
+  uint32_t* h_abort = nullptr;
   // host-mapped work FIFO (comm/mod.rs MCCS_WORK_FIFO_DEPTH) + done counters
   mccsDevWork* h_work = nullptr;
   mccsDevWork* d_work = nullptr;
@@ -297,6 +301,7 @@ mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream
 mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one
 int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live library comm's device struct, else 0
 void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
+mccsResult_t place_abort_line(Comm* c);     // the host-mapped abort line
 int comm_pool_count(unsigned generation);
 int comm_pool_waiting(unsigned generation);  // pooled arenas still awaiting a peer's release (tests)             // arenas pooled under that runtime (tests)
 // gate.cpp

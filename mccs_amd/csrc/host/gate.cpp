@@ -175,8 +175,8 @@ mccsResult_t gate_allreduce(std::vector<Comm*>& cs, std::vector<Buf>& bufs, size
     if (want_algo == MCCS_ALGO_RING || (sr != mccsTimeout && sr != mccsRemoteError)) return sr;
     MCCS_LOG("node gate: a direct AllReduce (algo %d) hit the watchdog on rank %d; voting it off", want_algo, c->rank);
     DeviceGuard g(c->device);
-    const uint32_t zero[2] = {0, 0};
-    MCCS_HIP(rt().Memcpy(c->d_abort, zero, sizeof(zero), hipMemcpyHostToDevice));
+    __atomic_store_n(c->h_abort + 1, 0u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(c->h_abort, 0u, __ATOMIC_SEQ_CST);
     c->failed = false;
     hung[k] = true;
   }

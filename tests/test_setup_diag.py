@@ -74,19 +74,20 @@ def _occurrences(trace):
 
 
 # (call, occurrence) -> the step mccsGetLastErrorString must name.  The
-# default config has 4 channels at 2 ranks: Malloc 1 = abort line, 2 = device
-# comm, 3..10 = per-channel peer / user-rank tables.
+# default config has 4 channels at 2 ranks: Malloc 1 = device comm, 2..9 =
+# per-channel peer / user-rank tables; HostMallocMapped 1 = the abort line.
 STEP = {("GetDeviceCount", 1): "make_comm",
         ("Memset", 1): "comm_alloc_local > FIFO arena zero-fill",
         ("FlushCaches", 1): "comm_alloc_local > FIFO arena zero-fill",
         ("DeviceSynchronize", 1): "comm_alloc_local > FIFO arena zero-fill",
-        ("Memset", 2): "comm_alloc_local > device comm",
-        ("HostMallocMapped", 1): "comm_alloc_local > work FIFO",
-        ("HostGetDevicePointer", 1): "comm_alloc_local > work FIFO",
-        ("HostMallocMapped", 2): "comm_alloc_local > graph work arena",
-        ("HostGetDevicePointer", 2): "comm_alloc_local > graph work arena",
-        ("HostMallocMapped", 3): "comm_alloc_local > work done counters",
-        ("HostGetDevicePointer", 3): "comm_alloc_local > work done counters",
+        ("HostMallocMapped", 1): "comm_alloc_local > abort line",
+        ("HostGetDevicePointer", 1): "comm_alloc_local > abort line",
+        ("HostMallocMapped", 2): "comm_alloc_local > work FIFO",
+        ("HostGetDevicePointer", 2): "comm_alloc_local > work FIFO",
+        ("HostMallocMapped", 3): "comm_alloc_local > graph work arena",
+        ("HostGetDevicePointer", 3): "comm_alloc_local > graph work arena",
+        ("HostMallocMapped", 4): "comm_alloc_local > work done counters",
+        ("HostGetDevicePointer", 4): "comm_alloc_local > work done counters",
         ("EventCreate", 1): "comm_alloc_local > events",
         ("EventCreate", 2): "comm_alloc_local > events"}
 STEP.update({("Malloc", k): "comm_alloc_local > device comm" for k in range(1, 11)})
@@ -229,7 +230,7 @@ def test_peer_setup_failure_reaches_every_rank(lib):
         C.init_communicator_rank(0, 2, 0, exchange)
     # the failing rank's own exception carries its diagnosis
     _fresh(lib)
-    lib.mccs_test_fake_fail(b"HostMallocMapped", 2, OOM)
+    lib.mccs_test_fake_fail(b"HostMallocMapped", 3, OOM)
     sent = {}
 
     def exchange2(mine):
@@ -271,7 +272,7 @@ def test_init_all_failure_names_the_rank_and_step(lib):
     """mccsCommInitAll (one process driving every GPU): a failure in the
     second rank's setup names that rank and step, and frees the first rank."""
     _fresh(lib)
-    lib.mccs_test_fake_fail(b"HostMallocMapped", 4, OOM)  # rank 1's work FIFO (3 per rank)
+    lib.mccs_test_fake_fail(b"HostMallocMapped", 6, OOM)  # rank 1's work FIFO (4 per rank: abort line first)
     comms = (ctypes.c_void_p * 2)()
     devs = (ctypes.c_int * 2)(0, 1)
     cfg, keep = C.CommConfig().to_c(2)
