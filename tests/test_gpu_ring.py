@@ -503,64 +503,70 @@ def test_allreduce_captured_in_hip_graph(orc, n, count, bridge, fifo, monkeypatc
 
 
 def test_graph_recapture_reuses_the_work_arena(orc, monkeypatch):
-    """A server that captures graphs again and again: 600 captures of a
-    grouped AllReduce whose works go through the graph work arena (more
-    entries than the arena's 2048), each graph destroyed after use, so its
-    entries return (a HIP user object the graph retains).  A graph captured
-    first and kept keeps its entries through all of them: torch destroys the
-    captured graph right after instantiation, so this also checks that the
-    executable graph holds the user object."""
+    """A server that captures graphs again and again: 150 captures of a group
+    of 40 int32 AllReduces (4 chained works on each of 4 channels per rank:
+    2,400 arena entries in all, more than the arena's 2048), each graph
+    destroyed after use, so its entries return (a HIP user object the graph
+    retains).  A graph captured first and kept keeps its entries through all
+    of them: torch destroys the captured graph right after instantiation, so
+    this also checks that the executable graph holds the user object."""
     import gc
 
     import torch
 
     monkeypatch.setenv("MCCS_INLINE_WORKS", "0")  # every captured launch takes arena entries
-    n, count = 2, 1 << 18
+    n = 2
     comms = C.init_all([0] * n, C.CommConfig(buffer_size=1 << 20, timeout_ms=10000))
     try:
         rng = np.random.default_rng(5)
         s = torch.cuda.Stream()
+        count = 1 << 18  # fp16 for the kept graph
+        kept_send = [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)]
+        kept_recv = [torch.empty_like(x) for x in kept_send]
+        with C.group():  # warm-up outside capture
+            for r in range(n):
+                C.all_reduce(comms[r], kept_send[r], kept_recv[r], count, F16, 0, stream=s)
+        s.synchronize()
 
-        def bufs():
-            return ([torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)],
-                    [torch.empty(count, dtype=torch.float16, device="cuda") for _ in range(n)])
+        def replay_kept():
+            inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
+            for r in range(n):
+                kept_send[r].copy_(torch.from_numpy(inputs[r]).cuda())
+            torch.cuda.synchronize()
+            kept.replay()
+            torch.cuda.synchronize()
+            exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0], buff_size=1 << 20)
+            _check_all_equal([kept_recv[r].cpu().numpy() for r in range(n)], exp, F16)
 
-        def capture(send, recv):
+        kept = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(kept, stream=s):
+            with C.group():
+                for r in range(n):
+                    C.all_reduce(comms[r], kept_send[r], kept_recv[r], count, F16, 0, stream=s)
+        replay_kept()
+        # the throwaway graphs: 40 int32 AllReduces of 4 MiB per rank in one group
+        m, icount = 40, 1 << 20
+        assert C.task_schema(icount * 4, comms[0].nchannels)[0] == comms[0].nchannels == 4
+        isend = [torch.full((icount,), 2042 + r, dtype=torch.int32, device="cuda") for r in range(n)]
+        irecv = [[torch.empty(icount, dtype=torch.int32, device="cuda") for _ in range(m)] for _ in range(n)]
+        for i in range(150):  # 150 x 4 channels x ceil(40 / 10) works = 2,400 entries per rank
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 with C.group():
-                    for r in range(n):
-                        C.all_reduce(comms[r], send[r], recv[r], count, F16, 0, stream=s)
-            return g
-
-        def replay_and_check(g, send, recv):
-            inputs = [vnode.gen(F16, count, rng) for _ in range(n)]
-            for r in range(n):
-                send[r].copy_(torch.from_numpy(inputs[r]).cuda())
-            torch.cuda.synchronize()
-            g.replay()
-            torch.cuda.synchronize()
-            exp = vnode.expected_allreduce(orc, inputs, F16, 0, comms[0], buff_size=1 << 20)
-            _check_all_equal([recv[r].cpu().numpy() for r in range(n)], exp, F16)
-
-        with C.group():  # warm-up outside capture
-            for r in range(n):
-                C.all_reduce(comms[r], *[b[r] for b in bufs()], count, F16, 0, stream=s)
-        s.synchronize()
-        kept_send, kept_recv = bufs()
-        kept = capture(kept_send, kept_recv)
-        replay_and_check(kept, kept_send, kept_recv)
-        send, recv = bufs()
-        per = C.task_schema(count * 2, comms[0].nchannels)[0]  # channels (= arena entries) per capture
-        assert 600 * per > 2048
-        for i in range(600):
-            g = capture(send, recv)
-            if i % 100 == 99:
-                replay_and_check(g, send, recv)
+                    for k in range(m):
+                        for r in range(n):
+                            C.all_reduce(comms[r], isend[r], irecv[r][k], icount, I32, 0, stream=s)
+            if i % 50 == 49:
+                for r in range(n):
+                    for k in range(m):
+                        irecv[r][k].zero_()
+                g.replay()
+                torch.cuda.synchronize()
+                assert all(bool((irecv[r][k] == 2042 * 2 + 1).all()) for r in range(n) for k in range(m)), i
             del g
             gc.collect()
         torch.cuda.synchronize()
-        replay_and_check(kept, kept_send, kept_recv)
+        replay_kept()
         del kept
     finally:
         torch.cuda.synchronize()
