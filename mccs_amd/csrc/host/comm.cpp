@@ -174,26 +174,51 @@ static size_t arena_class(size_t need) {
   return (need + g - 1) / g * g;
 }
 
-// Clears the bits of the peers whose release word now holds the epoch
-// (g_pool_mu held).  True when nothing is awaited.
-static bool pool_released(PooledArena& a) {
-  if (!a.waiting) return true;
-  uint64_t w[ArenaLayout::kReleaseBytes / sizeof(uint64_t)];
-  if (rt().Memcpy(w, a.ptr + a.release_off, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) return false;
-  for (int r = 0; r < 64; ++r)
-    if ((a.waiting >> r & 1) && w[r] == a.epoch) a.waiting &= ~(1ull << r);
-  return a.waiting == 0;
+// Reads the release words of the pooled arenas `pick` selects that still
+// await a peer, and clears the bits of the peers whose word now holds the
+// tenancy's epoch.  The copies run outside g_pool_mu: a device copy can queue
+// behind a running kernel, and other threads' setups must not wait on that.
+// An entry taken or re-pooled meanwhile is matched by (ptr, epoch), which no
+// later tenancy repeats.
+template <class Pick>
+static void pool_refresh(Pick pick) {
+  struct Check {
+    char* ptr;
+    size_t off;
+    uint64_t epoch, waiting;
+  };
+  std::vector<Check> todo;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (const auto& a : g_pool)
+      if (a.waiting && a.generation == rt_generation() && pick(a)) todo.push_back({a.ptr, a.release_off, a.epoch, a.waiting});
+  }
+  if (todo.empty()) return;
+  for (auto& t : todo) {
+    uint64_t w[ArenaLayout::kReleaseBytes / sizeof(uint64_t)];
+    uint64_t released = 0;
+    if (rt().Memcpy(w, t.ptr + t.off, sizeof(w), hipMemcpyDeviceToHost) == hipSuccess)
+      for (int r = 0; r < 64; ++r)
+        if ((t.waiting >> r & 1) && w[r] == t.epoch) released |= 1ull << r;
+    t.waiting = released;
+  }
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (auto& a : g_pool)
+    for (const auto& t : todo)
+      if (a.ptr == t.ptr && a.epoch == t.epoch) a.waiting &= ~t.waiting;
 }
 
 static char* pool_take(int device, bool uncached, size_t need, size_t* got) {
+  auto fits = [&](const PooledArena& a) {
+    return a.generation == rt_generation() && a.device == device && a.uncached == uncached && a.bytes >= need &&
+           a.bytes <= 2 * need;
+  };
+  pool_refresh(fits);
   std::lock_guard<std::mutex> lk(g_pool_mu);
   size_t best = g_pool.size();
-  for (size_t i = 0; i < g_pool.size(); ++i) {
-    PooledArena& a = g_pool[i];
-    if (a.generation == rt_generation() && a.device == device && a.uncached == uncached && a.bytes >= need &&
-        a.bytes <= 2 * need && (best == g_pool.size() || a.bytes < g_pool[best].bytes) && pool_released(a))
+  for (size_t i = 0; i < g_pool.size(); ++i)
+    if (fits(g_pool[i]) && !g_pool[i].waiting && (best == g_pool.size() || g_pool[i].bytes < g_pool[best].bytes))
       best = i;
-  }
   if (best == g_pool.size()) return nullptr;
   char* p = g_pool[best].ptr;
   *got = g_pool[best].bytes;
@@ -216,11 +241,12 @@ static void pool_give(int device, bool uncached, size_t bytes, char* p, uint64_t
 static size_t pool_release_uncached(int device) {
   std::vector<char*> drop;
   size_t bytes = 0;
+  pool_refresh([&](const PooledArena& a) { return a.device == device && a.uncached; });
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     for (size_t i = 0; i < g_pool.size();)
       if (g_pool[i].generation == rt_generation() && g_pool[i].device == device && g_pool[i].uncached &&
-          pool_released(g_pool[i])) {
+          !g_pool[i].waiting) {
         drop.push_back(g_pool[i].ptr);
         bytes += g_pool[i].bytes;
         g_pool.erase(g_pool.begin() + i);
@@ -275,9 +301,10 @@ int comm_pool_count(unsigned generation) {
 }
 
 int comm_pool_waiting(unsigned generation) {
+  if (generation == rt_generation()) pool_refresh([](const PooledArena&) { return true; });
   std::lock_guard<std::mutex> lk(g_pool_mu);
   int n = 0;
-  for (auto& a : g_pool) n += a.generation == generation && !pool_released(a);
+  for (const auto& a : g_pool) n += a.generation == generation && a.waiting != 0;
   return n;
 }
 
