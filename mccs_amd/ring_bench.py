@@ -617,6 +617,31 @@ def host_record() -> dict:
     return rec
 
 
+def gpu_bus_id(device: int) -> str:
+    """PCI bus id of a visible device ("ordinal:N" if the runtime will not
+    say): device ordinals are local to a process, bus ids are not."""
+    import ctypes
+
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 63, device) == 0 and buf.value:
+            return buf.value.decode()
+    except OSError:
+        pass
+    return f"ordinal:{device}"
+
+
+def ranks_share_gpu(dist, device: int, world: int, group=None) -> bool:
+    """Whether two ranks of `group` drive the same physical GPU (a 1-GPU
+    rehearsal), from their PCI bus ids -- not from this process's device
+    count, which per-rank device visibility (HIP_VISIBLE_DEVICES) would make
+    1 on a full node."""
+    ids = [None] * world
+    dist.all_gather_object(ids, gpu_bus_id(device), group=group)
+    return len(set(ids)) < world
+
+
 def cpu_ring_baseline(world: int, nbytes: int, nchannels: int, budget_s: float = 4.0) -> dict:
     """SURVEY §8(d) configs[2]: the same ring schedule run by host threads
     over host memory (mccs_host_ring_allreduce: `world` ranks x `nchannels`
@@ -778,7 +803,7 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
         return lambda: C.all_reduce(cm, x, y, n, code, C.AllReduceOpType.Sum, stream)
 
     tune_table = None
-    share = ndev < world
+    share = ranks_share_gpu(dist, device, world)
     rejected = []
     t = budget.clock()
     if getattr(args, "no_autotune", False):
@@ -848,7 +873,7 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
     dist.barrier()
     if extra and os.environ.get("MCCS_BENCH_NO_REFDRV") != "1":
         extras["reference_driven"] = budget.run(
-            "reference_driven", lambda: reference_driven_leg(torch, dist, rank, world, device, nbytes))
+            "reference_driven", lambda: reference_driven_leg(torch, dist, rank, world, device, nbytes, share))
     calib = None
     if extra and budget.allow("node_legs"):
         # rank 0 alone drives every GPU; ranks 1..N-1 wait at the barrier below
@@ -884,7 +909,7 @@ def _run_ring(args, torch, dist, C, rank, world, device, dev, ndev, cpu_sum_base
                      ranks_share_gpu=share, cpu_baseline=cpu, extras=extras, calibration=calib)
 
 
-def reference_driven_leg(torch, dist, rank, world, device, nbytes) -> dict:
+def reference_driven_leg(torch, dist, rank, world, device, nbytes, share=None) -> dict:
     """The depth-A drop-in timed on this node (mccs_amd/refdrive.py): the
     reference-named kernels driven exactly as plan.rs drives them, for the
     configurations an unchanged Rust service selects by configuration alone.
@@ -895,7 +920,8 @@ def reference_driven_leg(torch, dist, rank, world, device, nbytes) -> dict:
     t0 = time.perf_counter()
     # ranks sharing one GPU (a rehearsal): every rank's one-workgroup-per-
     # channel kernel must be resident at once, so keep them to half the CUs
-    share = torch.cuda.device_count() < world
+    if share is None:
+        share = ranks_share_gpu(dist, device, world)
     max_ch = max(2, 128 // world) if share else 32
     try:
         # a hang on a bad node ends in 20 s, not the kernels' 10 min default
@@ -975,7 +1001,7 @@ def setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, warmup
     name, count = SETUP2_JOBS[job]
     nbytes, compute_us, _ = traffic.SETUP2[name]
     assert nbytes == 2 * count
-    share = torch.cuda.device_count() < world  # a 1-GPU rehearsal: every process on one GPU
+    share = ranks_share_gpu(dist, device, world)  # a 1-GPU rehearsal: every process on one GPU
     modes = _candidates(C, [shared_gpu_lanes(world) if share and "MCCS_LANES" not in os.environ else None],
                         [None])[0][1]
     comm, mode = make_validated_comm(torch, dist, C, jrank, half, device, dev, _exchange_factory(dist, half, grp),
@@ -1086,7 +1112,7 @@ def run_setup2(args, torch, dist, C, rank, world, device, dev, interleaved=False
     larger job's buckets (4 x setup-2_vgg fp16, sampled)."""
     scale = float(os.environ.get("MCCS_SETUP2_COMPUTE_SCALE", "1.0"))
     res = setup2_measure(torch, dist, C, rank, world, device, dev, interleaved, args.warmup, args.steps, scale)
-    share = torch.cuda.device_count() < world
+    share = ranks_share_gpu(dist, device, world)
     if rank != 0:
         dist.barrier()
         return None

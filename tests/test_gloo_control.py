@@ -247,3 +247,44 @@ def test_bench_budget_skips_a_leg_on_every_rank():
         assert ran == ["a", "c"], (rank, ran)
         assert legs["b"]["skipped"] == "budget" and legs["b"]["need_s"] == 10
         assert "wall_s" in legs["a"] and "wall_s" in legs["c"]
+
+
+def _share_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from mccs_amd import ring_bench as rb
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = []
+        # a full node with per-rank device visibility: each process sees ONE
+        # device, ordinal 0, yet the bus ids differ -> not sharing
+        rb.gpu_bus_id = lambda dev: f"0000:{0x10 + rank:02x}:00.0"
+        out.append(rb.ranks_share_gpu(dist, 0, world))
+        # a 1-GPU rehearsal: every rank on the same bus id -> sharing
+        rb.gpu_bus_id = lambda dev: "0000:75:00.0"
+        out.append(rb.ranks_share_gpu(dist, 0, world))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_decides_gpu_sharing_from_bus_ids():
+    """The N > 1 line prices ranks that share a GPU against HBM and spreads
+    their lanes; whether they do comes from the ranks' PCI bus ids, not from
+    how many devices one process sees (1 under per-rank HIP_VISIBLE_DEVICES
+    on a full node)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_share_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [[False, True], [False, True]]
