@@ -117,6 +117,26 @@ def test_allreduce_ops(orc, op, code):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("n", [3, 5, 8])
+@pytest.mark.parametrize("code", [F16, BF16])
+def test_allreduce_prod_half_types(orc, n, code):
+    """Prod in fp16 / bf16 through the ring: products of n values in [-1, 1)
+    reach fp16 subnormals (below 6.1e-5) and round at every hop, so the
+    per-hop rounding and subnormal handling must match the oracle bit for bit
+    (the reference keeps subnormals: no fast-math, reduce_kernel.h:287-309)."""
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(17 * n + code)
+        inputs = [vnode.gen(code, 100003, rng) for _ in range(n)]
+        outs = vnode.run_allreduce(comms, inputs, code, 1)
+        exp = vnode.expected_allreduce(orc, inputs, code, 1, comms[0])
+        _check_all_equal(outs, exp, code)
+        if code == F16:  # the case is not vacuous
+            assert np.count_nonzero(np.abs(exp.astype(np.float32)) < 6.1e-5) > 100
+    finally:
+        vnode.destroy(comms)
+
+
 @pytest.mark.parametrize("code", list(range(10)))
 @pytest.mark.parametrize("op", [0, 2])
 def test_allreduce_every_dtype(orc, code, op):

@@ -24,7 +24,7 @@ def _case(seed):
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 9))
     code = int(rng.choice([0, 2, 4, 6, 7, 8, 9]))
-    op = int(rng.choice([0, 0, 0, 1, 2, 3])) if code not in (6, 9) else int(rng.choice([0, 0, 2, 3]))
+    op = int(rng.choice([0, 0, 0, 1, 2, 3]))
     esize = vnode.ESIZE[code]
     count = int(rng.choice([1, 3, 127, 4096 + 3, int(rng.integers(1, 1 << 20)), (1 << 22) // esize + 77]))
     cfg = {}

@@ -44,7 +44,7 @@ def sequence(rng, nops):
         code = int(rng.choice([0, 2, 4, 6, 7, 8, 9]))
         count = max(1, int(np.exp(rng.uniform(0, np.log(MAX_BYTES)))) // vnode.ESIZE[code])
         if u < 0.7:
-            op = int(rng.choice([0, 0, 0, 1, 2, 3])) if code not in (6, 9) else int(rng.choice([0, 0, 2, 3]))
+            op = int(rng.choice([0, 0, 0, 1, 2, 3]))
             ops.append(dict(kind="ar", code=code, op=op, count=count, inplace=bool(rng.random() < 0.25)))
         elif u < 0.85:
             ops.append(dict(kind="ag", nbytes=count * vnode.ESIZE[code]))
