@@ -234,3 +234,40 @@ def test_reduce_beyond_2pow31_elements():
     mccs_amd.reduce(c, [a, b])
     torch.cuda.synchronize()
     assert torch.equal(c, a + b)
+
+
+@pytest.mark.parametrize("code", [6, 7, 8, 9])
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+@pytest.mark.parametrize("nsrcs", [2, 3])
+def test_reduce_nan_and_inf(orc, code, op, nsrcs):
+    """NaN / +-Inf (2 % each) in every source: the per-type operators of
+    reduce_kernel.h decide what survives (float / double Max/Min
+    (x < y) ? y : x keep a NaN first operand and drop a NaN second one; half and
+    bf16 go through fmaxf / fminf, which drop either).  NaN positions match
+    the oracle's and every other element is bit-exact (payloads not compared)."""
+    rng = np.random.default_rng(7 * code + op + 100 * nsrcs)
+    n = 50021
+    srcs = []
+    for _ in range(nsrcs):
+        x = rand(code, n, rng)
+        u = rng.random(n)
+        if code == 9:  # bf16 bit patterns
+            x[u < 0.02] = 0x7FC0
+            x[(u >= 0.02) & (u < 0.04)] = 0x7F80
+            x[(u >= 0.04) & (u < 0.06)] = 0xFF80
+        else:
+            x[u < 0.02] = np.nan
+            x[(u >= 0.02) & (u < 0.04)] = np.inf
+            x[(u >= 0.04) & (u < 0.06)] = -np.inf
+        srcs.append(x)
+    (got,) = run_reduce(srcs, 1, code, op)
+    (ref,) = orc.reduce_copy(code, op, srcs)
+
+    def isnan(a):
+        if code == 9:
+            return np.isnan((a.view(np.uint16).astype(np.uint32) << 16).view(np.float32))
+        return np.isnan(a)
+
+    assert np.array_equal(isnan(got), isnan(ref))
+    keep = ~isnan(ref)
+    assert np.array_equal(got.view(np.uint8).reshape(n, -1)[keep], ref.view(np.uint8).reshape(n, -1)[keep])

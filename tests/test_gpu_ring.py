@@ -137,6 +137,52 @@ def test_allreduce_prod_half_types(orc, n, code):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+@pytest.mark.parametrize("code", [F32, F16, BF16, F64])
+def test_allreduce_nan_and_inf(orc, code, op):
+    """NaN and +-Inf inputs (1 % each) through the ring at n = 3: the
+    reference's per-type operators decide what survives -- float / double
+    Max/Min are (x < y) ? y : x, so a NaN second operand is dropped; half and
+    bf16 Max/Min go through fmaxf / fminf, which drop either NaN
+    (reduce_kernel.h:32-46,338-404) -- and Inf - Inf makes NaN in Sum.  The NaN
+    positions must match the oracle's and every other element bit for bit
+    (NaN payloads are not compared: the reference's hardware makes its own)."""
+    n, count = 3, 65537
+    comms = C.init_all([0] * n)
+    try:
+        rng = np.random.default_rng(31 * code + op)
+        inputs = []
+        for _ in range(n):
+            x = vnode.gen(code, count, rng)
+            f = x.view(np.uint16) if code == BF16 else x
+            special = rng.random(count)
+            if code == BF16:  # bf16 bit patterns: NaN 0x7fc0, +Inf 0x7f80, -Inf 0xff80
+                f[special < 0.01] = 0x7FC0
+                f[(special >= 0.01) & (special < 0.02)] = 0x7F80
+                f[(special >= 0.02) & (special < 0.03)] = 0xFF80
+            else:
+                f[special < 0.01] = np.nan
+                f[(special >= 0.01) & (special < 0.02)] = np.inf
+                f[(special >= 0.02) & (special < 0.03)] = -np.inf
+            inputs.append(x)
+        outs = vnode.run_allreduce(comms, inputs, code, op)
+        exp = vnode.expected_allreduce(orc, inputs, code, op, comms[0])
+
+        def as_float(a):
+            if code == BF16:
+                return (a.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+            return a.astype(np.float64)
+
+        en = np.isnan(as_float(exp))
+        assert en.any() or op in (2, 3)
+        for r, o in enumerate(outs):
+            on = np.isnan(as_float(o))
+            assert np.array_equal(on, en), (r, np.flatnonzero(on != en)[:8])
+            assert np.array_equal(o.view(np.uint8).reshape(count, -1)[~en], exp.view(np.uint8).reshape(count, -1)[~en]), r
+    finally:
+        vnode.destroy(comms)
+
+
 @pytest.mark.parametrize("code", list(range(10)))
 @pytest.mark.parametrize("op", [0, 2])
 def test_allreduce_every_dtype(orc, code, op):
