@@ -505,3 +505,41 @@ def test_ll_several_words_per_thread(orc, monkeypatch, inplace):
         _check(outs, vnode.expected_allreduce(orc, inputs, F32, 0, comms[0]))
     finally:
         vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("code", [F32, F16, BF16])
+@pytest.mark.parametrize("op", [0, 2, 3])
+def test_direct_nan_and_inf(orc, code, op, variant):
+    """NaN / +-Inf inputs through each direct kernel: the same per-type
+    operators as the ring (float Max/Min (x < y) ? y : x, half/bf16 fmaxf),
+    so the NaN positions and every other bit equal the ring's (the oracle)."""
+    n, count = 3, 30011
+    comms = C.init_all([0] * n, _cfg(variant))
+    try:
+        rng = np.random.default_rng(13 * code + op)
+        inputs = []
+        for _ in range(n):
+            x = vnode.gen(code, count, rng)
+            f = x.view(np.uint16) if code == BF16 else x
+            u = rng.random(count)
+            if code == BF16:
+                f[u < 0.02], f[(u >= 0.02) & (u < 0.04)], f[(u >= 0.04) & (u < 0.06)] = 0x7FC0, 0x7F80, 0xFF80
+            else:
+                f[u < 0.02], f[(u >= 0.02) & (u < 0.04)], f[(u >= 0.04) & (u < 0.06)] = np.nan, np.inf, -np.inf
+            inputs.append(x)
+        outs = vnode.run_allreduce(comms, inputs, code, op)
+        _algo(comms, variant, inputs[0].nbytes)
+        exp = vnode.expected_allreduce(orc, inputs, code, op, comms[0])
+
+        def isnan(a):
+            if code == BF16:
+                return np.isnan((a.view(np.uint16).astype(np.uint32) << 16).view(np.float32))
+            return np.isnan(a.astype(np.float64))
+
+        en = isnan(exp)
+        for r, o in enumerate(outs):
+            assert np.array_equal(isnan(o), en), r
+            assert np.array_equal(o.view(np.uint8).reshape(count, -1)[~en], exp.view(np.uint8).reshape(count, -1)[~en]), r
+    finally:
+        vnode.destroy(comms)
