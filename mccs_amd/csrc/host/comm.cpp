@@ -622,6 +622,13 @@ hipError_t comm_wait_last_launch(Comm* c) {
   return rt().DeviceSynchronize();  // nothing recorded the launch: every stream of the device
 }
 
+hipError_t comm_order_after_last_launch(Comm* c, hipStream_t s) {
+  if (c->event_recorded) return rt().StreamWaitEvent(s, c->event);
+  std::lock_guard<std::mutex> lk(g_live_mu);  // the owner's event: read while it cannot be replaced or freed
+  if (c->sync_owner && g_live_comms.count(c->sync_owner)) return rt().StreamWaitEvent(s, c->sync_owner->event);
+  return hipSuccess;
+}
+
 mccsResult_t comm_free(Comm* c) {
   DeviceGuard g(c->device);
   // the last launch (any stream) must be done before its arenas are reused

@@ -254,6 +254,10 @@ struct Comm {
   // The owner's event is read at wait time (under the live-comm lock), so an
   // owner that replaces its event (comm_make_event_ipc) leaves no dangling copy.
   Comm* sync_owner = nullptr;
+  // The stream the comm's latest launch went to (plan_launch_group orders a
+  // launch on another stream after it).
+  hipStream_t last_stream = nullptr;
+  bool launched = false;
   // Threads synchronizing on this comm's event outside the live-comm lock
   // (comm_wait_last_launch): the event is not destroyed or replaced while > 0.
   std::atomic<int> waiters{0};
@@ -296,6 +300,8 @@ mccsResult_t comm_build_device(Comm* c);
 void default_rings(int nranks, int nch_req, std::vector<std::vector<int>>* rings);
 mccsResult_t comm_free(Comm* c);
 hipError_t comm_wait_last_launch(Comm* c);  // host wait for the comm's latest launch
+// Makes stream `s` wait for the comm's latest launch (none recorded: no-op).
+hipError_t comm_order_after_last_launch(Comm* c, hipStream_t s);
 mccsResult_t comm_set_kernel_cfg(Comm* c);
 mccsResult_t comm_stream(Comm* c, hipStream_t* out);  // creates the comm stream on first use
 mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm event to an interprocess one

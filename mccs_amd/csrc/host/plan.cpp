@@ -685,6 +685,18 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
         MCCS_HIP(rt().StreamWaitEvent(st, c->user_event));
       }
     }
+    // A communicator's launches run one at a time in issue order, as on the
+    // reference's private comm stream (proxy/init.rs:166-175): its kernels
+    // share the FIFO flags, the lanes' saved steps and the direct counters.
+    // A launch on another stream than the comm's previous one therefore waits
+    // for that launch first (two launches of one comm on two streams ran
+    // concurrently and returned wrong sums, 2 of 6 cases at n = 4).  Not while
+    // capturing: a graph cannot depend on an event recorded outside it.
+    if (!capturing)
+      for (size_t k = 0; k < idx.size(); ++k) {
+        Comm* c = comms[idx[k]];
+        if (c->launched && c->last_stream != st) MCCS_HIP(comm_order_after_last_launch(c, st));
+      }
     // The launching comm's event rides on the dispatch's own completion signal
     // (hipExtLaunchKernel stopEvent): a hipEventRecord behind the kernel is a
     // marker packet that cost ~3 us of device time per launch on MI355X, the
@@ -710,6 +722,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     if (record)
       for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
     for (size_t k = 0; k < idx.size(); ++k) {
+      comms[idx[k]]->last_stream = st;
+      comms[idx[k]]->launched = true;
       comms[idx[k]]->event_recorded = record;
       // fused rank slots without their own record wait on the launching comm's event
       comms[idx[k]]->sync_owner = (k > 0 && !record && stop_on_launch) ? c0 : nullptr;

@@ -639,6 +639,42 @@ def test_graph_recapture_reuses_the_work_arena(orc, monkeypatch):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("rep", range(3))
+def test_one_comm_on_two_streams_runs_in_issue_order(orc, n, rep):
+    """A large AllReduce on one stream, then a small one on another, same
+    communicators, no sync between: the second must wait for the first (the
+    reference runs a communicator's kernels on its one private stream,
+    proxy/init.rs:166-175).  Launched concurrently they shared FIFO flags and
+    saved steps and returned wrong sums in 2 of 6 of these cases at n = 4."""
+    import torch
+
+    comms = C.init_all([0] * n, C.CommConfig(timeout_ms=5000, lanes=1, channel_count=1))
+    try:
+        rng = np.random.default_rng(3 + rep)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        cnt_a, cnt_b = 16 << 20, 1 << 18
+        xa = [vnode.gen(F32, cnt_a, rng) for _ in range(n)]
+        xb = [vnode.gen(F32, cnt_b, rng) for _ in range(n)]
+        sa, sb = [vnode.to_dev(x) for x in xa], [vnode.to_dev(x) for x in xb]
+        ra, rb = [torch.zeros_like(t) for t in sa], [torch.zeros_like(t) for t in sb]
+        torch.cuda.synchronize()
+        for stream, cnt, snd, rcv in ((s1, cnt_a, sa, ra), (s2, cnt_b, sb, rb)):
+            with C.group():
+                for r in range(n):
+                    C.all_reduce(comms[r], snd[r], rcv[r], cnt, F32, 0, stream=stream)
+        torch.cuda.synchronize()
+        for c in comms:
+            c.sync()
+        ea = vnode.expected_allreduce(orc, xa, F32, 0, comms[0])
+        eb = vnode.expected_allreduce(orc, xb, F32, 0, comms[0])
+        _check_all_equal([ra[r].cpu().numpy() for r in range(n)], ea, F32)
+        _check_all_equal([rb[r].cpu().numpy() for r in range(n)], eb, F32)
+    finally:
+        torch.cuda.synchronize()
+        vnode.destroy(comms)
+
+
 @pytest.mark.parametrize("code,off", [(F16, 2), (F32, 4), (F32, 12), (BF16, 6)])
 def test_allreduce_misaligned_buffers(orc, code, off):
     """User buffers that are not 16-byte aligned take the typed element path

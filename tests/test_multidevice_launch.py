@@ -579,3 +579,36 @@ def test_fused_rank_sync_waits_on_the_launch_not_the_device(fake):
     finally:
         for c in (comms[1], comms[3]):
             c.destroy()
+
+
+def test_launch_on_another_stream_waits_for_the_previous_one(fake):
+    """A communicator's launches run in issue order whatever stream each one
+    is issued on (the reference runs them on one private stream,
+    proxy/init.rs:166-175): a launch on another stream than the comm's
+    previous one waits for that launch's event first; on the same stream the
+    stream order is enough and nothing is added."""
+    fake(2)
+    comms = C.init_all([0, 1], C.CommConfig(buffer_size=1 << 20))
+    try:
+        def group(stream):
+            with C.group():
+                for r, c in enumerate(comms):
+                    C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 1 << 20, F32, SUM,
+                                 stream=stream)
+
+        group(0x7000)
+        _log()
+        group(0x7000)  # same stream: no wait
+        assert not any(k == "stream_wait" for k, _ in _log())
+        group(0x7100)  # another stream: waits for the previous launch on every device
+        ev = _log()
+        waits = [kv for k, kv in ev if k == "stream_wait"]
+        assert sorted(int(kv["dev"]) for kv in waits) == [0, 1], ev
+        assert all(kv["stream"] == str(0x7100) and kv["event_dev"] == kv["dev"] for kv in waits), waits
+        for d in (0, 1):  # on each device the wait is queued before that device's launch
+            w = next(i for i, (k, kv) in enumerate(ev) if k == "stream_wait" and kv["dev"] == str(d))
+            l = next(i for i, (k, kv) in enumerate(ev) if k == "launch" and kv["dev"] == str(d))
+            assert w < l, ev
+    finally:
+        for c in comms:
+            c.destroy()
