@@ -192,7 +192,13 @@ mccsResult_t mccsCommSetupRank(mccsComm_t *comm, int rank, int nranks, int devic
 mccsResult_t mccsCommConnect(mccsComm_t comm, const void *all_handles);
 
 /* libmccs::all_reduce (src/libmccs/src/collectives.rs:75-138): count in
- * elements of dtype, stream-ordered on `stream`, returns after launch. */
+ * elements of dtype, stream-ordered on `stream`, returns after launch.
+ * A communicator's collectives run in the order they are issued, whatever
+ * stream each is issued on (a launch on another stream than the comm's
+ * previous one waits for it), as on the reference's one private comm stream.
+ * Calls on ONE communicator must come from one thread at a time (group state
+ * is per thread); different communicators may be driven from different
+ * threads at once. */
 mccsResult_t mccsAllReduce(const void *sendbuff, void *recvbuff, size_t count, int dtype, int op, mccsComm_t comm,
                            hipStream_t stream);
 /* libmccs::all_gather: sendbytes per rank; recvbuff holds nranks*sendbytes. */
