@@ -127,6 +127,67 @@ def test_random_collective_sequence(orc, seed):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("seed", range(CASES))
+def test_random_collective_sequence_mixed_streams(orc, seed):
+    """The same kind of sequence with every collective issued on one of three
+    streams at random: a communicator's launches still run in issue order
+    (a launch on another stream waits for the previous one), so every output
+    equals the oracle's.  Inputs are staged and synchronised first: data
+    dependencies across streams are the caller's, launch order is the
+    library's."""
+    import torch
+
+    rng = np.random.default_rng(11000 + seed)
+    n = int(rng.integers(2, 9))
+    comms = C.init_all([0] * n)
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream(), torch.cuda.Stream()]
+    try:
+        staged = []  # (kind, code, op, count/nbytes, host inputs, send, recv)
+        for o in sequence(rng, OPS):
+            if o["kind"] == "ar":
+                xs = [vnode.gen(o["code"], o["count"], rng) for _ in range(n)]
+                send = [vnode.to_dev(x) for x in xs]
+                recv = send if o["inplace"] else [vnode.to_dev(np.zeros_like(x)) for x in xs]
+                staged.append([("ar", o["code"], o["op"], o["count"], xs, send, recv)])
+            elif o["kind"] == "ag":
+                xs = [rng.integers(0, 256, o["nbytes"], dtype=np.uint8) for _ in range(n)]
+                staged.append([("ag", None, None, o["nbytes"], xs, [vnode.to_dev(x) for x in xs],
+                                [vnode.to_dev(np.zeros(n * o["nbytes"], np.uint8)) for _ in range(n)])])
+            else:
+                batch = []
+                for count in o["counts"]:
+                    xs = [vnode.gen(o["code"], count, rng) for _ in range(n)]
+                    batch.append(("group", o["code"], o["op"], count, xs, [vnode.to_dev(x) for x in xs],
+                                  [vnode.to_dev(np.zeros_like(x)) for x in xs]))
+                staged.append(batch)
+        torch.cuda.synchronize()
+        for item in staged:
+            st = streams[int(rng.integers(0, 3))]
+            with C.group():
+                for kind, code, op, cnt, xs, send, recv in item:
+                    for r in range(n):
+                        if kind == "ag":
+                            C.all_gather(comms[r], send[r], recv[r], cnt, stream=st)
+                        else:
+                            C.all_reduce(comms[r], send[r], recv[r], cnt, code, op, stream=st)
+        torch.cuda.synchronize()
+        for c in comms:
+            c.sync()
+        for item in staged:
+            for kind, code, op, cnt, xs, send, recv in item:
+                if kind == "ag":
+                    exp = orc.ring_allgather(xs)
+                elif kind == "ar":
+                    exp = vnode.expected_allreduce(orc, xs, code, op, comms[0])
+                else:
+                    exp = _int_allreduce(xs, op)
+                for r in range(n):
+                    got = recv[r].cpu().numpy() if kind == "ag" else vnode.from_dev(recv[r], code)
+                    assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (seed, n, kind, code, op, cnt, r)
+    finally:
+        vnode.destroy(comms)
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_random_sequence_graph_replay(orc, seed):
     """The whole sequence captured into one HIP graph and replayed three
