@@ -59,11 +59,13 @@ def ddp_stream(comm, rank, world, orc, vnode):
     return out
 
 
-def seq_stream(comm, rank, world, orc, vnode, nops=40):
+def seq_stream(comm, rank, world, orc, vnode, nops=40, streams=False):
     """tests/test_gpu_sequence_fuzz.py's random collective sequence (same
     list on every rank), issued back to back on this rank's communicator at
     the library's default routing, one sync at the end, every output checked
-    against the oracle."""
+    against the oracle.  streams: each collective on one of three streams,
+    drawn per rank (the stream waits for the current one, where the inputs
+    were copied; the library orders the comm's launches across streams)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -73,6 +75,15 @@ def seq_stream(comm, rank, world, orc, vnode, nops=40):
 
     seq = sequence(np.random.default_rng(9000 + world), nops)
     rng = np.random.default_rng(77 + rank)
+    srng = np.random.default_rng(500 + rank)
+    pool = [torch.cuda.current_stream(), torch.cuda.Stream(), torch.cuda.Stream()]
+
+    def stream():
+        if not streams:
+            return None
+        st = pool[int(srng.integers(0, 3))]
+        st.wait_stream(torch.cuda.current_stream())  # the inputs were copied on the current stream
+        return st
 
     def gathered(x):
         xs = [None] * world
@@ -86,7 +97,7 @@ def seq_stream(comm, rank, world, orc, vnode, nops=40):
             xs = gathered(x)
             send = vnode.to_dev(x)
             recv = send if o["inplace"] else vnode.to_dev(np.zeros_like(x))
-            C.all_reduce(comm, send, recv, o["count"], o["code"], o["op"])
+            C.all_reduce(comm, send, recv, o["count"], o["code"], o["op"], stream())
             algos.add(comm.last_algo())
             p = vnode.Planner(comm.nchannels, comm.rings())
             nch, nthr, rings = p.select(x.nbytes, 0)
@@ -97,16 +108,17 @@ def seq_stream(comm, rank, world, orc, vnode, nops=40):
             xs = gathered(x)
             send = vnode.to_dev(x)
             recv = vnode.to_dev(np.zeros(world * o["nbytes"], np.uint8))
-            C.all_gather(comm, send, recv, o["nbytes"])
+            C.all_gather(comm, send, recv, o["nbytes"], stream())
             checks.append((f"{i}/ag/b{o['nbytes']}", recv, orc.ring_allgather(xs), None))
         else:
             batch = []
             for count in o["counts"]:
                 x = vnode.gen(o["code"], count, rng)
                 batch.append((count, gathered(x), vnode.to_dev(x), vnode.to_dev(np.zeros_like(x))))
+            st = stream()
             with C.group():
                 for count, xs, send, recv in batch:
-                    C.all_reduce(comm, send, recv, count, o["code"], o["op"])
+                    C.all_reduce(comm, send, recv, count, o["code"], o["op"], st)
             for k, (count, xs, send, recv) in enumerate(batch):
                 checks.append((f"{i}.{k}/group/code{o['code']}/op{o['op']}/n{count}", recv,
                                _int_allreduce(xs, o["op"]), o["code"]))
@@ -154,7 +166,8 @@ def main():
                  # the library defaults, fed a DDP-style bucket stream (vnode.DDP_STREAM)
                  "ddp": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
                  # tests/test_gpu_sequence_fuzz.py's random sequence at the defaults
-                 "seq": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
+                 "seq": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
+                 "seqs": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
     direct_kw = {"direct": dict(direct_bytes=8 << 20, oneshot_bytes=-1, ll_bytes=-1),
                  "oneshot": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=-1),
                  "ll": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=1 << 20)}
@@ -169,8 +182,11 @@ def main():
         comm = C.init_communicator_rank(rank, world, dev, exchange,
                                         C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, lanes=lanes,
                                                      **direct_kw.get(mode, {})))
-        if mode in ("ddp", "seq"):
-            results.update((ddp_stream if mode == "ddp" else seq_stream)(comm, rank, world, orc, vnode))
+        if mode in ("ddp", "seq", "seqs"):
+            if mode == "ddp":
+                results.update(ddp_stream(comm, rank, world, orc, vnode))
+            else:
+                results.update(seq_stream(comm, rank, world, orc, vnode, streams=mode == "seqs"))
             dist.barrier()  # every rank's last kernel is done before any arena returns to the pool
             comm.destroy()
             continue

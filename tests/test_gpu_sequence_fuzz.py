@@ -251,11 +251,11 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_random_collective_sequence_across_processes(world):
+@pytest.mark.parametrize("world,mode", [(2, "seq"), (3, "seq"), (4, "seq"), (2, "seqs"), (4, "seqs")])
+def test_random_collective_sequence_across_processes(world, mode):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(HERE, "ipc_worker.py")]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", IPC_MODES="seq")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", IPC_MODES=mode)  # seqs: random streams per call
     for k in ("MCCS_ONESHOT_BYTES", "MCCS_DIRECT_BYTES", "MCCS_LL_BYTES"):
         env.pop(k, None)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=os.path.dirname(HERE))
