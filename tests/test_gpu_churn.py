@@ -30,7 +30,7 @@ DIRECT_DEFAULTS = True  # conftest: keep the library defaults (the LL bucket bel
 HERE = os.path.dirname(os.path.abspath(__file__))
 INT32, SUM = 2, 0
 DRIFT_BYTES = 128 << 20  # one leaked arena per cycle would be >= 1 MiB x 36 cycles, mostly far more
-SHAPES, ROUNDS = 12, 4
+SHAPES, ROUNDS = 12, int(os.environ.get("MCCS_CHURN_ROUNDS", "4"))
 
 
 def churn_shapes(seed, nshapes, n_choices):
