@@ -240,6 +240,9 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld, hipGraph_t graph)
     }
   if (chan_list.empty()) return mccsInternalError;
   uint32_t start = 0;
+  if (work_count > Comm::kGraphWorkEntries)
+    MCCS_FAIL(mccsInvalidUsage, "one captured launch needs %u work entries, more than the graph work arena's %u: "
+              "split the group", work_count, Comm::kGraphWorkEntries);
   if (!c->graph_pool->take(work_count, &start))
     MCCS_FAIL(mccsInvalidUsage, "graph work arena exhausted (%u of %u entries held by live graphs, %u needed)",
               c->graph_pool->held_now(), Comm::kGraphWorkEntries, work_count);
@@ -321,6 +324,12 @@ static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
       work_count += (uint32_t)c->sched[ch].works.size();
     }
   if (chan_list.empty()) return mccsInternalError;
+  // one launch's works must fit the ring at once (they are all read by the
+  // one kernel): more could never be acknowledged, and the wait below would
+  // spin until it mistook the idle stream for a dead kernel
+  if (work_count > c->work_depth)
+    MCCS_FAIL(mccsInvalidUsage, "one launch needs %u work entries, more than the work FIFO's %u: split the group "
+              "or raise mccsCommConfig.work_fifo_depth", work_count, c->work_depth);
   const uint32_t qmask = c->work_depth - 1;
   const uint32_t nchan = (uint32_t)chan_list.size();
   uint32_t first = c->work_next;

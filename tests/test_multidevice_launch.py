@@ -612,3 +612,27 @@ def test_launch_on_another_stream_waits_for_the_previous_one(fake):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_launch_larger_than_the_work_fifo_is_refused(fake, monkeypatch):
+    """A group whose works cannot all sit in the work FIFO at once (the one
+    kernel reads them all) is refused up front with the reason, instead of
+    waiting for acknowledgements that cannot come."""
+    from mccs_amd._lib import MccsError
+
+    monkeypatch.setenv("MCCS_INLINE_WORKS", "0")
+    fake(2)
+    comms = C.init_all([0, 1], C.CommConfig(buffer_size=1 << 20, work_fifo_depth=8))
+    try:
+        with pytest.raises(MccsError, match="more than the work FIFO's 8: split the group"):
+            with C.group():
+                for _ in range(25):  # 25 elements per channel: 3 chained works on each of 4 channels = 12
+                    for r, c in enumerate(comms):
+                        C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 1 << 20, F32, SUM,
+                                     stream=0)
+        _log()
+        _allreduce_group(comms)  # the comms stay usable
+        assert sum(1 for k, _ in _log() if k == "launch") == 2
+    finally:
+        for c in comms:
+            c.destroy()
