@@ -286,9 +286,9 @@ static int inline_channels(const Comm* c) {
   if (v && std::atoi(v) == 0) return 0;
   int used = 0;
   for (int ch = 0; ch < c->nch; ++ch) {
-    const size_t w = c->sched[ch].works.size();
-    if (w > 1) return 0;
-    used += w == 1;
+    const auto& works = c->sched[ch].works;
+    if (works.size() > 1 || (works.size() == 1 && works[0].size() != 1)) return 0;  // one work of one element
+    used += works.size() == 1;
   }
   return used;
 }
@@ -299,7 +299,9 @@ static mccsResult_t upload_work_inline(Comm* c, LaunchDesc* ld, mccsMultiLaunchA
   for (int ch = 0; ch < c->nch; ++ch)
     if (!c->sched[ch].works.empty()) {
       mask |= 1ull << ch;
-      ma->inline_work[ma->inline_works + n++] = to_dev_work(c->sched[ch].works[0], false, true, 0);
+      const mccsDevWork w = to_dev_work(c->sched[ch].works[0], false, true, 0);
+      ma->inline_work[ma->inline_works + n].header = w.header;
+      ma->inline_work[ma->inline_works + n++].elem = w.elems[0];
     }
   ma->inline_works += n;
   ld->mask = mask;

@@ -68,13 +68,20 @@ struct mccsRingKernelCfg {
 // launch (several when ranks share a GPU: tests' virtual node).
 // blockIdx.y = rank slot.
 #define MCCS_MULTI_MAX_RANKS 16
-// A launch whose ranks' channels each run one work may carry those works in
-// its arguments (kernarg memory is device memory on MI355X) instead of the
-// host-mapped work FIFO, whose read over PCIe is the long pole of the kernel
-// prologue; inFifo = 0, so nothing is acknowledged.  Rank slot k's works are
-// inline_work[k * channels used ...].  7 works = the n = 8 rings and keeps the
-// arguments under 4 KiB.
+// A launch whose ranks' channels each run one work of one element may carry
+// those works in its arguments (kernarg memory is device memory on MI355X)
+// instead of the host-mapped work FIFO, whose read over PCIe is the long pole
+// of the kernel prologue; inFifo = 0, so nothing is acknowledged.  Rank slot
+// k's works are inline_work[k * channels used ...], each only its header and
+// its one element (mccsInlineWork, 56 B instead of mccsDevWork's 512): HIP
+// copies every argument byte at every launch, and 4 KiB of them cost 1-3 us
+// of host time per launch (profiles/r05_host_overhead.json).  7 works = the
+// n = 8 rings.
 #define MCCS_INLINE_WORKS 7
+struct mccsInlineWork {
+  struct mccsDevWorkHeader header;
+  struct mccsDevWorkElem elem;
+};
 // The connector addresses one channel's lanes need (the prev recv and next
 // send mccsDevConnInfo fields), kept by this library beside its device
 // communicator (comm.cpp comm_build_device): a launch loads them together with
@@ -96,10 +103,12 @@ struct mccsMultiLaunchArgs {
   struct mccsRingKernelCfg cfg;  // this launch's hand-off policy
   uint32_t inline_works;         // > 0: the works are inline_work[0 .. inline_works)
   uint32_t pad3[3];
-  struct mccsDevWork inline_work[MCCS_INLINE_WORKS];
+  struct mccsInlineWork inline_work[MCCS_INLINE_WORKS];
 };
 #ifdef __cplusplus
-static_assert(sizeof(mccsMultiLaunchArgs) <= 4096, "ring launch arguments must stay within 4 KiB");
+static_assert(sizeof(mccsInlineWork) == 56 && offsetof(mccsInlineWork, elem) == offsetof(mccsDevWork, elems),
+              "an inline work is the head of a mccsDevWork: header + one element");
+static_assert(sizeof(mccsMultiLaunchArgs) <= 1024, "ring launch arguments must stay within 1 KiB");
 #endif
 
 // ---- Direct AllReduce on a fully connected node (direct_kernel.h)

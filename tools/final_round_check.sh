@@ -4,11 +4,12 @@
 # N = 8 lines, the N = 4 line with the node gate forced on every connect as on
 # a node, configs[3] and configs[4] standalone, and a 5 s budget that must skip
 # legs yet still print the line).  Each step under its own limit; stops at the
-# first step that faults or times out (tools/gpu_step.sh).
+# first step that faults or times out (tools/gpu_step.sh).  SKIP_TESTS=1 skips
+# the suite (when it ran in a call of its own).
 rm -f gpurun_out/steps.log
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 S=tools/gpu_step.sh
-$S tests 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread || exit 1
+[ -n "$SKIP_TESTS" ] || $S tests 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread || exit 1
 $S smoke 200 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 $S n1 200 python bench.py || exit 1
 $S r_n2 400 $TR --nproc-per-node 2 --master-port 29871 bench.py --gpus 2 || exit 1
