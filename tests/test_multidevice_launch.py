@@ -166,7 +166,7 @@ def test_connector_views_match_the_peers(fake, n):
 def test_work_list_falls_back_to_the_fifo(fake, monkeypatch):
     """Works go through the reference's work FIFO when they do not fit the
     launch arguments: several collectives of a group on one channel (chained
-    works), or MCCS_INLINE_WORKS=0."""
+    works, or one work of several elements), or MCCS_INLINE_WORKS=0."""
     fake(8)
     comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
     try:
@@ -175,6 +175,15 @@ def test_work_list_falls_back_to_the_fifo(fake, monkeypatch):
             # 12 grouped 4 MiB AllReduces, each on all 7 channels: 12 elements per
             # channel = 2 chained works (MCCS_MAX_WORK_ELEMENTS = 10 per work)
             for _ in range(12):
+                for r, c in enumerate(comms):
+                    C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 1 << 20, F32, SUM,
+                                 stream=0)
+        launches = [kv for k, kv in _log() if k == "launch"]
+        assert len(launches) == 8 and all(kv["inline_works"] == "0" for kv in launches), launches
+        # two grouped AllReduces: one work per channel, but of two elements; an
+        # inline work carries its header and ONE element (ring_cfg.h mccsInlineWork)
+        with C.group():
+            for _ in range(2):
                 for r, c in enumerate(comms):
                     C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 1 << 20, F32, SUM,
                                  stream=0)
