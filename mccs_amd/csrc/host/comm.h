@@ -256,7 +256,7 @@ struct Comm {
   Comm* sync_owner = nullptr;
   // The stream the comm's latest launch went to (plan_launch_group orders a
   // launch on another stream after it).
-  hipStream_t last_stream = nullptr;
+  unsigned long long last_stream_id = 0;  // DeviceRuntime::StreamId of the latest launch's stream
   bool launched = false;
   // Threads synchronizing on this comm's event outside the live-comm lock
   // (comm_wait_last_launch): the event is not destroyed or replaced while > 0.

@@ -703,10 +703,14 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     // for that launch first (two launches of one comm on two streams ran
     // concurrently and returned wrong sums, 2 of 6 cases at n = 4).  Not while
     // capturing: a graph cannot depend on an event recorded outside it.
+    // Streams are told apart by id, not address: a stream destroyed with the
+    // comm's kernel still queued gives its address to the next one created.
+    unsigned long long st_id = 0;
+    MCCS_HIP(rt().StreamId(st, &st_id));
     if (!capturing)
       for (size_t k = 0; k < idx.size(); ++k) {
         Comm* c = comms[idx[k]];
-        if (c->launched && c->last_stream != st) MCCS_HIP(comm_order_after_last_launch(c, st));
+        if (c->launched && c->last_stream_id != st_id) MCCS_HIP(comm_order_after_last_launch(c, st));
       }
     // The launching comm's event rides on the dispatch's own completion signal
     // (hipExtLaunchKernel stopEvent): a hipEventRecord behind the kernel is a
@@ -733,7 +737,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     if (record)
       for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
     for (size_t k = 0; k < idx.size(); ++k) {
-      comms[idx[k]]->last_stream = st;
+      comms[idx[k]]->last_stream_id = st_id;
       comms[idx[k]]->launched = true;
       comms[idx[k]]->event_recorded = record;
       // fused rank slots without their own record wait on the launching comm's event

@@ -3,6 +3,7 @@
 // GPUs.
 #include "rt.h"
 
+#include <dlfcn.h>
 #include <hip/hip_ext.h>
 
 #include <algorithm>
@@ -85,6 +86,20 @@ class HipRuntime final : public DeviceRuntime {
   hipError_t StreamDestroy(hipStream_t s) override { return ret(hipStreamDestroy(s)); }
   hipError_t StreamSynchronize(hipStream_t s) override { return ret(hipStreamSynchronize(s)); }
   hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) override { return ret(hipStreamWaitEvent(s, e, 0)); }
+  // hipStreamGetId is a ROCm 7.1 symbol: resolved at run time, since the
+  // process may already hold an older libamdhip64 (torch's own, ROCm 7.0, on
+  // this image).  Without it the stream's address stands in for its id; torch
+  // never destroys its streams (a per-device pool), so there addresses do not
+  // come back as new streams.
+  hipError_t StreamId(hipStream_t s, unsigned long long* id) override {
+    using Fn = hipError_t (*)(hipStream_t, unsigned long long*);
+    static const Fn fn = (Fn)dlsym(RTLD_DEFAULT, "hipStreamGetId");
+    if (!fn) {
+      *id = (unsigned long long)(uintptr_t)s;
+      return hipSuccess;
+    }
+    return ret(fn(s, id));
+  }
   hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) override {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     hipError_t e = hipStreamIsCapturing(s, &st);
@@ -297,6 +312,19 @@ class FakeRuntime final : public DeviceRuntime {
          std::to_string((uintptr_t)e) + " event_dev=" + std::to_string(event_dev(e)));
     return hipSuccess;
   }
+  hipError_t StreamId(hipStream_t s, unsigned long long* id) override {
+    if (hipError_t e = inj("StreamId")) return e;
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = stream_ids_.find(s);
+    if (it == stream_ids_.end()) it = stream_ids_.emplace(s, ++next_stream_id_).first;
+    *id = it->second;
+    return hipSuccess;
+  }
+  // A stream destroyed and created again at the same address: a new id.
+  void recreate_stream(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stream_ids_.erase(s);
+  }
   hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) override {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -503,6 +531,8 @@ class FakeRuntime final : public DeviceRuntime {
   std::map<std::string, Fail> fail_;
   std::map<std::string, int> delay_ms_;
   std::map<hipStream_t, int> capture_;
+  std::map<hipStream_t, unsigned long long> stream_ids_;
+  unsigned long long next_stream_id_ = 0;
   std::map<int, std::vector<std::pair<void (*)(void*), void*>>> on_destroy_;
   std::ostringstream log_, calls_;
 };
@@ -619,6 +649,15 @@ extern "C" int mccs_test_fake_delay(const char* call, int ms) {
 
 // Marks the fake stream `stream` (a handle value as the library's callers
 // pass it) as capturing into graph id `graph` (> 0), or ends its capture (0).
+// Simulates hipStreamDestroy + hipStreamCreate returning the same address.
+extern "C" int mccs_test_fake_recreate_stream(void* stream) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  f->recreate_stream((hipStream_t)stream);
+  return 0;
+}
+
 extern "C" int mccs_test_fake_capture(void* stream, int graph) {
   std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
   mccs::FakeRuntime* f = mccs::g_fake.load();

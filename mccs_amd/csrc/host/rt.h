@@ -46,6 +46,10 @@ class DeviceRuntime {
   virtual hipError_t StreamDestroy(hipStream_t s) = 0;
   virtual hipError_t StreamSynchronize(hipStream_t s) = 0;
   virtual hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) = 0;
+  // A stream's process-unique id: HIP hands a destroyed stream's address to
+  // the next stream it creates (tools/stream_id_probe.c), so the address does
+  // not tell two streams apart; the id does.
+  virtual hipError_t StreamId(hipStream_t s, unsigned long long* id) = 0;
   virtual hipError_t StreamIsCapturing(hipStream_t s, bool* capturing) = 0;
   // The graph a capturing stream records into, and a host callback run once
   // that graph and every executable graph instantiated from it are destroyed

@@ -623,6 +623,36 @@ def test_launch_on_another_stream_waits_for_the_previous_one(fake):
             c.destroy()
 
 
+def test_recreated_stream_at_the_same_address_is_another_stream(fake):
+    """HIP gives a destroyed stream's address to the next stream created
+    (tools/stream_id_probe.c: six create/destroy rounds, one address, ids
+    2..7), and a stream destroyed with work still queued keeps running it.  So
+    a comm's next launch on a new stream at the old address must still wait
+    for the previous launch: streams are compared by id, not address."""
+    fake(2)
+    comms = C.init_all([0, 1], C.CommConfig(buffer_size=1 << 20))
+    lib = _lib.load()
+    lib.mccs_test_fake_recreate_stream.argtypes = [ctypes.c_void_p]
+    try:
+        def group(stream):
+            with C.group():
+                for r, c in enumerate(comms):
+                    C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 1 << 20, F32, SUM,
+                                 stream=stream)
+
+        group(0x7000)
+        _log()
+        group(0x7000)
+        assert not any(k == "stream_wait" for k, _ in _log())
+        assert lib.mccs_test_fake_recreate_stream(0x7000) == 0
+        group(0x7000)  # same address, new stream: waits on every device
+        waits = [kv for k, kv in _log() if k == "stream_wait"]
+        assert sorted(int(kv["dev"]) for kv in waits) == [0, 1], waits
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_launch_larger_than_the_work_fifo_is_refused(fake, monkeypatch):
     """A group whose works cannot all sit in the work FIFO at once (the one
     kernel reads them all) is refused up front with the reason, instead of
