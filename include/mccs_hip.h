@@ -196,6 +196,16 @@ mccsResult_t mccsCommConnect(mccsComm_t comm, const void *all_handles);
  * A communicator's collectives run in the order they are issued, whatever
  * stream each is issued on (a launch on another stream than the comm's
  * previous one waits for it), as on the reference's one private comm stream.
+ * Exception: a collective captured into a HIP graph runs when the graph is
+ * replayed, and a replay makes no library call, so it is not ordered against
+ * the comm's other launches by issue.  Instead every launch of a communicator,
+ * replayed or not, takes the communicator's launch guard on the GPU before it
+ * touches the comm's FIFO state, so two of its kernels never run at once: a
+ * replay and a launch on another stream with no dependency between them run
+ * one after the other, in either order.  Across processes each rank decides
+ * that order on its own, so ranks whose replays race other launches of the
+ * comm must order those streams themselves (a captured and an eager collective
+ * of the same shape could otherwise pair up differently on different ranks).
  * Calls on ONE communicator must come from one thread at a time (group state
  * is per thread); different communicators may be driven from different
  * threads at once. */
@@ -256,6 +266,16 @@ int mccsCommDirectEnabled(mccsComm_t comm);
 #define MCCS_GATE_TWOSHOT 0x20      /* two-shot */
 #define MCCS_GATE_NO_ATOMICS 0x40   /* some rank cannot perform peer atomics (direct kernel off) */
 mccsResult_t mccsCommGateInfo(mccsComm_t comm, int *info4);
+/* The comm's launch guard (inspection, tests): out4[0] the token of the launch
+ * holding it (0 = free), [1] 1 once a fused launch holds every rank slot's
+ * guard, [2] workgroups of the holder that have finished, [3] workgroups that
+ * ever found it held by another launch of the comm and waited.  Copies from
+ * device memory (synchronous). */
+mccsResult_t mccsCommGuardInfo(mccsComm_t comm, uint64_t *out4);
+/* 1 when this process's HIP runtime tells streams apart by hipStreamGetId,
+ * 0 when by address (a runtime older than ROCm 7.1 loaded first, e.g. torch's).
+ * The cross-stream issue order above keys on it. */
+int mccs_stream_id_native(void);
 /* Device pointer of the comm's mccsDevCommAndChannels (for inspection). */
 mccsResult_t mccsCommDevComm(mccsComm_t comm, void **dev_comm);
 const char *mccsGetErrorString(mccsResult_t r);

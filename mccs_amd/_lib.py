@@ -116,6 +116,8 @@ SIGNATURES: dict[str, tuple] = {
     "mccs_ll_default": (_c_int, [_c_int]),
     "mccsCommDirectEnabled": (_c_int, [_c_void_p]),
     "mccsCommGateInfo": (_c_int, [_c_void_p, _P(_c_int)]),
+    "mccsCommGuardInfo": (_c_int, [_c_void_p, _P(ctypes.c_uint64)]),
+    "mccs_stream_id_native": (_c_int, []),
     "mccs_ring_profile": (_c_int, [_c_int, _P(ctypes.c_ulonglong), _c_int]),
     "mccsMemAllocShared": (_c_int, [_c_int, _c_size_t, _P(_c_void_p), _c_void_p]),
     "mccsMemFreeShared": (_c_int, [_c_int, _c_void_p]),

@@ -149,6 +149,15 @@ class Communicator:
         _lib.check(_sig().mccsCommGateInfo(self._h, info), "mccsCommGateInfo")
         return {"ran": bool(info[0]), "fifo_mode": info[1], "failed": info[2], "disabled": info[3]}
 
+    def guard_info(self) -> dict:
+        """The comm's launch guard (mccsCommGuardInfo, launch_guard.h): the
+        holder's token (0 = free), the fused-launch confirm word, finished
+        workgroups of the holder, and how many workgroups ever waited for
+        another launch of this comm."""
+        out = (ctypes.c_uint64 * 4)()
+        _lib.check(_sig().mccsCommGuardInfo(self._h, out), "mccsCommGuardInfo")
+        return {"owner": out[0], "confirm": out[1], "fin": out[2], "waits": out[3]}
+
     def rings(self) -> list[list[int]]:
         out = []
         for ch in range(self.nchannels):

@@ -704,8 +704,36 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
 
 template <int DT, int OP>
 __global__ void __launch_bounds__(MCCS_DIRECT_THREADS) direct_kernel(mccsDirectArgs a) {
+  // Launch guard (launch_guard.h), taken before the prologue reads the
+  // control block's launch count and running totals.  The rank slots' fields
+  // are read where the kernel arguments live (taking the parameter's address
+  // would copy all 4 KiB of it to scratch); the guard's state waits out the
+  // body in LDS.
+  __shared__ GuardSlot s_guard;
+  if (threadIdx.x == 0) {
+    mccsLaunchGuard* g = nullptr;
+    int ok = 1;
+    if (!a.no_guard) {
+      const uintptr_t ka = (uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+      const mccsDirectRank* ranks = (const mccsDirectRank*)(ka + offsetof(mccsDirectArgs, r));
+      GuardWait w{};
+      w.abortFlagRef = (uint32_t* const*)&ranks[blockIdx.y].abort_flag;
+      w.timeout = a.timeout_ticks;
+      w.err_line = ranks[blockIdx.y].err_line;
+      g = comm_guard(ranks[blockIdx.y].comm);
+      ok = guard_acquire([&](int k) { return comm_guard(ranks[k].comm); }, (int)gridDim.y, (int)blockIdx.y,
+                         a.guard_order, launch_token(), blockIdx.x == 0 && blockIdx.y == 0, w);
+    }
+    s_guard.g = ok ? g : nullptr;
+    s_guard.ok = ok;
+  }
+  __syncthreads();
+  if (!s_guard.ok) return;
   if (a.mode == MCCS_DIRECT_LL_ONE_SHOT || a.mode == MCCS_DIRECT_LL_AG) direct_ll_body<DT, OP>(a);
   else direct_body<DT, OP>(a);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && s_guard.g) guard_release(s_guard.g, gridDim.x);
 }
 
 }  // namespace mccs

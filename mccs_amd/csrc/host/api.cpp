@@ -649,6 +649,19 @@ extern "C" int mccsCommDirectEnabled(mccsComm_t comm) {
   return c && c->direct_ok && (c->layout.direct_slot > 0 || c->layout.oneshot_slot > 0 || c->layout.ll_slot > 0);
 }
 
+extern "C" mccsResult_t mccsCommGuardInfo(mccsComm_t comm, uint64_t* out4) {
+  Comm* c = (Comm*)comm;
+  if (!c || !out4 || !c->d_guard) return mccsInvalidArgument;
+  DeviceGuard g(c->device);
+  mccsLaunchGuard line;
+  MCCS_HIP(rt().Memcpy(&line, c->d_guard, sizeof(line), hipMemcpyDeviceToHost));
+  out4[0] = line.word >> MCCS_GUARD_TOK_SHIFT;
+  out4[1] = (line.word & MCCS_GUARD_CONFIRMED) ? 1 : 0;
+  out4[2] = line.word & MCCS_GUARD_FIN_MASK;
+  out4[3] = line.waits;
+  return mccsSuccess;
+}
+
 extern "C" mccsResult_t mccsCommDevComm(mccsComm_t comm, void** dev_comm) {
   Comm* c = (Comm*)comm;
   if (!c || !dev_comm) return mccsInvalidArgument;

@@ -130,6 +130,12 @@ mccsResult_t comm_set_kernel_cfg(Comm* c) {
   // communicator creation, carried in the connect handle: both ends agree).
   k.slice_steps = (uint32_t)c->slice_steps;
   if (const char* v = std::getenv("MCCS_RING_PROFILE")) k.profile = std::atoi(v) != 0;
+  // MCCS_LAUNCH_GUARD=0 (test hook, honoured only with MCCS_TEST_HOOKS=1, read
+  // when the comm connects): its launches skip the launch guard
+  // (launch_guard.h), so a test can show the overlap the guard prevents
+  const char* hooks = std::getenv("MCCS_TEST_HOOKS");
+  const char* guard = std::getenv("MCCS_LAUNCH_GUARD");
+  k.no_guard = hooks && std::atoi(hooks) == 1 && guard && std::atoi(guard) == 0;
   c->kcfg = k;  // travels in every launch's arguments (no device global)
   return mccsSuccess;
 }
@@ -458,9 +464,11 @@ mccsResult_t comm_alloc_local(Comm* c) {
   MCCS_CHECK(place_abort_line(c));
   {
     StepScope st("device comm");
-    MCCS_HIP(rt().Malloc((void**)&c->d_comm,
-                         sizeof(mccsDevCommAndChannels) + sizeof(mccsRingConnView) * MCCS_MAX_NCHANNELS));
+    // device communicator, per-channel views, launch guard (ring_cfg.h)
+    MCCS_HIP(rt().Malloc((void**)&c->d_comm, MCCS_GUARD_OFF + sizeof(mccsLaunchGuard)));
     c->d_view = (mccsRingConnView*)((char*)c->d_comm + sizeof(mccsDevCommAndChannels));
+    c->d_guard = (mccsLaunchGuard*)((char*)c->d_comm + MCCS_GUARD_OFF);
+    MCCS_HIP(rt().Memset(c->d_guard, 0, sizeof(mccsLaunchGuard)));
     for (int ch = 0; ch < c->nch; ++ch) {
       MCCS_HIP(rt().Malloc((void**)&c->d_peers[ch], sizeof(mccsDevChannelPeer) * c->nranks));
       MCCS_HIP(rt().Malloc((void**)&c->d_user_ranks[ch], sizeof(int) * c->nranks));

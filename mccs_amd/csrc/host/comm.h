@@ -208,6 +208,7 @@ struct Comm {
   std::vector<mccsDevChannelPeer*> d_peers;
   std::vector<int*> d_user_ranks;
   mccsRingConnView* d_view = nullptr;  // per channel, in d_comm's allocation after the channels
+  mccsLaunchGuard* d_guard = nullptr;  // launch guard (launch_guard.h), in d_comm's allocation at MCCS_GUARD_OFF
   // The abort line (word 0 abortFlag, word 1 error bits) in host-mapped memory:
   // the host reads and writes it with plain CPU accesses (comm.cpp
   // place_abort_line), kernels through d_abort.
@@ -308,8 +309,8 @@ mccsResult_t comm_make_event_ipc(Comm* c);             // switches the comm even
 int comm_fifo_slots_of(const void* d_comm);            // fifo_slots of a live library comm's device struct, else 0
 void comm_pool_drop_generation(unsigned generation);   // forgets arenas pooled under a removed fake runtime
 mccsResult_t place_abort_line(Comm* c);     // the host-mapped abort line
-int comm_pool_count(unsigned generation);
-int comm_pool_waiting(unsigned generation);  // pooled arenas still awaiting a peer's release (tests)             // arenas pooled under that runtime (tests)
+int comm_pool_count(unsigned generation);    // arenas pooled under that runtime (tests)
+int comm_pool_waiting(unsigned generation);  // pooled arenas still awaiting a peer's release (tests)
 // gate.cpp
 bool gate_wanted(bool distinct_gpus);
 int gate_env();  // MCCS_GATE: -1 unset, else its value

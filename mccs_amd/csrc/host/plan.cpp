@@ -211,6 +211,18 @@ static bool eager_events() {
   return on;
 }
 
+// Rank slots of a launch listed by the address of their comm's launch guard,
+// 4 bits each (launch_guard.h: every fused launch takes its guards in this
+// one order, so two of them never hold each other's).
+static uint64_t guard_order(const std::vector<Comm*>& comms, const std::vector<int>& idx) {
+  std::vector<int> k(idx.size());
+  for (size_t i = 0; i < k.size(); ++i) k[i] = (int)i;
+  std::sort(k.begin(), k.end(), [&](int a, int b) { return comms[idx[a]]->d_guard < comms[idx[b]]->d_guard; });
+  uint64_t order = 0;
+  for (size_t i = 0; i < k.size(); ++i) order |= (uint64_t)k[i] << (4 * i);
+  return order;
+}
+
 namespace {
 struct GraphWorkRelease {
   std::shared_ptr<GraphWorkPool> pool;
@@ -640,6 +652,8 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
                                               : direct_kernel_ptr(c0->plan_dtype, c0->plan_op);
       if (!fn) return mccsInvalidArgument;
       block = MCCS_DIRECT_THREADS;
+      da.guard_order = guard_order(comms, idx);
+      for (int i : idx) da.no_guard |= comms[i]->kcfg.no_guard;  // comm_set_kernel_cfg's test hook
       args[0] = &da;
     } else {
       std::memset(&ma, 0, sizeof(ma));
@@ -677,6 +691,7 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
                                    : std::max(ma.cfg.timeout_ticks, ck->kcfg.timeout_ticks);
         ma.cfg.profile |= ck->kcfg.profile;
       }
+      ma.guard_order = guard_order(comms, idx);
       fn = lds[0].multi_fn;
       grid = (unsigned)(lds[0].nch_used * c0->lanes);
       block = (unsigned)c0->block_threads;
@@ -702,9 +717,12 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     // A launch on another stream than the comm's previous one therefore waits
     // for that launch first (two launches of one comm on two streams ran
     // concurrently and returned wrong sums, 2 of 6 cases at n = 4).  Not while
-    // capturing: a graph cannot depend on an event recorded outside it.
-    // Streams are told apart by id, not address: a stream destroyed with the
-    // comm's kernel still queued gives its address to the next one created.
+    // capturing: a graph cannot depend on an event recorded outside it, and a
+    // replay makes no library call -- the device's launch guard
+    // (launch_guard.h) keeps replays from running beside any other launch of
+    // the comm.  Streams are told apart by id, not address: a stream destroyed
+    // with the comm's kernel still queued gives its address to the next one
+    // created.
     unsigned long long st_id = 0;
     MCCS_HIP(rt().StreamId(st, &st_id));
     if (!capturing)
@@ -737,17 +755,23 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     if (record)
       for (size_t k = 1; k < idx.size(); ++k) MCCS_HIP(rt().EventRecord(comms[idx[k]]->event, st));
     for (size_t k = 0; k < idx.size(); ++k) {
-      comms[idx[k]]->last_stream_id = st_id;
-      comms[idx[k]]->launched = true;
-      comms[idx[k]]->event_recorded = record;
-      // fused rank slots without their own record wait on the launching comm's event
-      comms[idx[k]]->sync_owner = (k > 0 && !record && stop_on_launch) ? c0 : nullptr;
+      // A capture launches nothing: the comm's latest launch, its stream and
+      // its event stay those of the last eager launch (letting a
+      // capture overwrite them let the next eager launch on a third stream skip
+      // its wait for that one).
+      if (!capturing) {
+        comms[idx[k]]->last_stream_id = st_id;
+        comms[idx[k]]->launched = true;
+        comms[idx[k]]->event_recorded = record;
+        // fused rank slots without their own record wait on the launching comm's event
+        comms[idx[k]]->sync_owner = (k > 0 && !record && stop_on_launch) ? c0 : nullptr;
+      }
       comms[idx[k]]->last_algo = !direct                            ? MCCS_ALGO_RING
                                  : da.mode == MCCS_DIRECT_TWO_SHOT ? MCCS_ALGO_DIRECT
                                  : da.mode == MCCS_DIRECT_LL_ONE_SHOT || da.mode == MCCS_DIRECT_LL_AG ? MCCS_ALGO_LL
                                                                    : MCCS_ALGO_ONESHOT;
     }
-    c0->event_recorded = record || stop_on_launch;
+    if (!capturing) c0->event_recorded = record || stop_on_launch;
   }
   return mccsSuccess;
 }

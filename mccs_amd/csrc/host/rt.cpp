@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -91,9 +92,20 @@ class HipRuntime final : public DeviceRuntime {
   // this image).  Without it the stream's address stands in for its id; torch
   // never destroys its streams (a per-device pool), so there addresses do not
   // come back as new streams.
+  using StreamIdFn = hipError_t (*)(hipStream_t, unsigned long long*);
+  static StreamIdFn stream_id_fn() {
+    static const StreamIdFn fn = (StreamIdFn)dlsym(RTLD_DEFAULT, "hipStreamGetId");
+    return fn;
+  }
   hipError_t StreamId(hipStream_t s, unsigned long long* id) override {
-    using Fn = hipError_t (*)(hipStream_t, unsigned long long*);
-    static const Fn fn = (Fn)dlsym(RTLD_DEFAULT, "hipStreamGetId");
+    const StreamIdFn fn = stream_id_fn();
+    static const bool logged = [&] {  // which key tells streams apart, once per process
+      if (std::getenv("MCCS_DEBUG"))
+        std::fprintf(stderr, "[mccs] streams told apart by %s\n",
+                     fn ? "hipStreamGetId" : "address (hipStreamGetId absent from the loaded HIP runtime)");
+      return true;
+    }();
+    (void)logged;
     if (!fn) {
       *id = (unsigned long long)(uintptr_t)s;
       return hipSuccess;
@@ -391,14 +403,17 @@ class FakeRuntime final : public DeviceRuntime {
                             : da->mode == MCCS_DIRECT_LL_AG       ? "ll-ag"
                                                                   : "twoshot") +
                 " gx=" + std::to_string(grid.x) + " llslot=" + std::to_string(da->ll_slot_bytes) +
-                " piece=" + std::to_string(da->piece) + " piece2=" + std::to_string(da->piece2) + " owned=";
+                " piece=" + std::to_string(da->piece) + " piece2=" + std::to_string(da->piece2) +
+                " guard_order=" + std::to_string(da->guard_order) + " no_guard=" + std::to_string(da->no_guard) +
+                " owned=";
         for (unsigned t = 0; t < da->nranks && t < MCCS_DIRECT_MAX_RANKS; ++t)
           extra += (t ? "," : "") + std::to_string(da->owned[t]);
       } else {
         const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
         for (unsigned k = 0; k < grid.y; ++k) on_dev = on_dev && dev_of(ma->comm[k]) == cur_;
         inl = ma->inline_works;
-        extra = " fence=" + std::to_string(ma->cfg.fence_mode);
+        extra = " fence=" + std::to_string(ma->cfg.fence_mode) + " guard_order=" + std::to_string(ma->guard_order) +
+                " no_guard=" + std::to_string(ma->cfg.no_guard);
       }
     }
     note("launch dev=" + std::to_string(cur_) + " grid=" + std::to_string(grid.x) + "x" + std::to_string(grid.y) +
@@ -569,6 +584,8 @@ void rt_use_fake(int ndevices) {
 
 unsigned rt_generation() { return g_generation.load(); }
 
+bool rt_stream_ids_native() { return HipRuntime::stream_id_fn() != nullptr; }
+
 }  // namespace mccs
 
 // ---- test-only C-ABI (tests/test_multidevice_launch.py) -------------------
@@ -647,9 +664,8 @@ extern "C" int mccs_test_fake_delay(const char* call, int ms) {
   return 0;
 }
 
-// Marks the fake stream `stream` (a handle value as the library's callers
-// pass it) as capturing into graph id `graph` (> 0), or ends its capture (0).
-// Simulates hipStreamDestroy + hipStreamCreate returning the same address.
+// Simulates hipStreamDestroy + hipStreamCreate returning the same address:
+// the fake stream `stream` gets a new id.
 extern "C" int mccs_test_fake_recreate_stream(void* stream) {
   std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
   mccs::FakeRuntime* f = mccs::g_fake.load();
@@ -658,6 +674,8 @@ extern "C" int mccs_test_fake_recreate_stream(void* stream) {
   return 0;
 }
 
+// Marks the fake stream `stream` (a handle value as the library's callers
+// pass it) as capturing into graph id `graph` (> 0), or ends its capture (0).
 extern "C" int mccs_test_fake_capture(void* stream, int graph) {
   std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
   mccs::FakeRuntime* f = mccs::g_fake.load();
@@ -680,3 +698,9 @@ extern "C" int mccs_test_fake_destroy_graph(int graph) {
 // Pooled FIFO arenas of the current runtime still awaiting a peer's release
 // (comm.cpp pool; tests of the release protocol).
 extern "C" int mccs_test_pool_waiting(void) { return mccs::comm_pool_waiting(mccs::rt_generation()); }
+
+// 1 when streams are told apart by hipStreamGetId (the loaded HIP runtime has
+// it: ROCm >= 7.1), 0 when by address (an older runtime, e.g. torch's ROCm 7.0
+// libamdhip64 loaded first).  plan.cpp orders a comm's launch on another stream
+// after its previous one by this key.
+extern "C" int mccs_stream_id_native(void) { return mccs::rt_stream_ids_native() ? 1 : 0; }

@@ -79,5 +79,6 @@ void rt_use_fake(int ndevices);
 // installed fake.  Memory pooled under one runtime is never handed out under
 // another; a removed fake's pooled arenas are dropped (its memory died with it).
 unsigned rt_generation();
+bool rt_stream_ids_native();  // the HIP runtime tells streams apart by hipStreamGetId (else by address)
 
 }  // namespace mccs

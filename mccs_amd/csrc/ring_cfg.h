@@ -53,8 +53,31 @@ struct mccsRingKernelCfg {
                           // one error channel, devcomm.h abortFlag)
   uint32_t fifo_slots;    // physical FIFO slots (power of two >= MCCS_BUFFER_SLOTS): slot = step % fifo_slots,
                           // a sender may run fifo_slots steps ahead; the reference has 8
-  uint32_t pad;
+  uint32_t no_guard;      // 1: skip the launch guard (test hook MCCS_LAUNCH_GUARD=0 only)
 };
+
+// ---- Launch guard (launch_guard.h): one launch of a communicator at a time.
+// A communicator's kernels share its FIFO flag lines, the lanes' saved steps
+// (word 1 above) and the direct control block, so two of its launches running
+// at once return wrong sums.  The host orders eager launches across streams
+// (plan.cpp), but a graph replay makes no library call; so every library
+// launch first takes its communicator's guard line on the device and gives it
+// back when its last workgroup is done.  The line lives in the communicator's
+// device allocation, after mccsDevCommAndChannels and the per-channel views.
+// One word holds the whole state, so each step is one atomic: the holder's
+// token in bits 17..63 (0 = free), bit 16 "every slot held" (fused launches),
+// bits 0..15 the holder's workgroups of this slot that have finished.
+#define MCCS_GUARD_FIN_MASK 0xffffull
+#define MCCS_GUARD_CONFIRMED (1ull << 16)
+#define MCCS_GUARD_TOK_SHIFT 17
+struct mccsLaunchGuard {
+  uint64_t word;   // token << MCCS_GUARD_TOK_SHIFT | confirmed | finished workgroups; 0 = free
+  uint64_t waits;  // workgroups that found the guard held by another launch (diagnostic, only grows)
+  uint64_t pad[14];
+};
+#define MCCS_GUARD_OFF                                                                                      \
+  ((sizeof(struct mccsDevCommAndChannels) + MCCS_MAX_NCHANNELS * sizeof(struct mccsRingConnView) + 127) / \
+   128 * 128)
 
 // Per-device ring profile counters (s_memrealtime ticks, 100 MHz), summed
 // over every slice of every workgroup while mccsRingKernelCfg.profile is set.
@@ -102,7 +125,8 @@ struct mccsMultiLaunchArgs {
   uint64_t channelMask;
   struct mccsRingKernelCfg cfg;  // this launch's hand-off policy
   uint32_t inline_works;         // > 0: the works are inline_work[0 .. inline_works)
-  uint32_t pad3[3];
+  uint32_t pad3;
+  uint64_t guard_order;          // rank slots by guard address, 4 bits each (launch_guard.h)
   struct mccsInlineWork inline_work[MCCS_INLINE_WORKS];
 };
 #ifdef __cplusplus
@@ -202,6 +226,9 @@ struct mccsDirectArgs {
   uint32_t mode;                              // MCCS_DIRECT_TWO_SHOT / ONE_SHOT / AG_ONE_SHOT
   uint32_t piece;                             // elements per piece of the scatter / gather phases
   uint32_t piece2;                            // elements per piece of the reduction phase
+  uint32_t no_guard;                          // 1: skip the launch guard (test hook only)
+  uint32_t pad2;
+  uint64_t guard_order;                       // rank slots by guard address, 4 bits each (launch_guard.h)
   uint64_t owned[MCCS_DIRECT_MAX_RANKS];      // elements of the walk's chunks each rank owns
   uint8_t idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];  // rank at ring index k of channel bid
 };

@@ -132,6 +132,77 @@ def seq_stream(comm, rank, world, orc, vnode, nops=40, streams=False):
     return out
 
 
+def _streams():
+    """Two streams on different hardware queues: HIP maps a process's streams
+    onto a few queues (GPU_MAX_HW_QUEUES, 4 here) and runs one queue's
+    kernels in order, so two streams of one priority may share a queue and
+    never overlap; a queue carries one priority, so these two cannot."""
+    import torch
+
+    return torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1)
+
+
+def guard_overlap(comm, rank, world, orc, vnode):
+    """A replay beside an eager launch of the same communicator, one rank per
+    process (test_gpu_launch_guard.py): each rank captures AllReduce(S -> RX)
+    in a graph on stream B, then issues AllReduce(S -> RY) on stream A and
+    replays the graph on B at once, no sync and no event between A and B.
+    Each rank serialises the two on its launch guard in whatever order its
+    GPU queues pick, so rank 0's eager launch may pair with rank 1's replay
+    (mccs_hip.h: across processes that order is the caller's to fix); both
+    collectives reduce the same send buffer with the same schedule, so every
+    pairing gives the oracle's sum -- a wrong one here means two launches of a
+    comm overlapped on one rank."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from mccs_amd import comm as C
+
+    out = {}
+    for kind, code, count in (("ring", 7, 4 << 20), ("ll", 6, 30001)):
+        rng = np.random.default_rng(700 + rank)
+        sa, sb = _streams()
+        x = vnode.gen(code, count, rng)
+        xs = [None] * world
+        dist.all_gather_object(xs, x)
+        s = vnode.to_dev(x)
+        rx, ry = torch.zeros_like(s), torch.zeros_like(s)
+        with torch.cuda.stream(sb):
+            C.all_reduce(comm, s, rx, count, code, 0, sb)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=sb):
+            C.all_reduce(comm, s, rx, count, code, 0, sb)
+        torch.cuda.synchronize()
+        comm.sync()
+        algo = comm.last_algo()
+        p = vnode.Planner(comm.nchannels, comm.rings())
+        nch, nthr, rings = p.select(count * vnode.ESIZE[code], 0)
+        exp = orc.ring_allreduce(code, 0, xs, nchannels=nch, nthreads=nthr, ring_orders=rings)
+        w0 = comm.guard_info()["waits"]
+        ok = True
+        for rep in range(4):
+            rx.zero_()
+            ry.zero_()
+            torch.cuda.synchronize()
+            dist.barrier()
+            C.all_reduce(comm, s, ry, count, code, 0, sa)
+            with torch.cuda.stream(sb):
+                g.replay()
+            torch.cuda.synchronize()
+            comm.sync()
+            for t in (rx, ry):
+                ok = ok and bool(np.array_equal(vnode.from_dev(t, code).view(np.uint8), exp.view(np.uint8)))
+        gi = comm.guard_info()
+        out[f"guard/{kind}/{algo}/exact"] = ok
+        out[f"guard/{kind}/idle"] = (gi["owner"], gi["confirm"], gi["fin"]) == (0, 0, 0)
+        print(json.dumps({"rank": rank, "kind": kind, "algo": algo, "waits": gi["waits"] - w0}), flush=True)
+        del g
+        torch.cuda.synchronize()
+    return out
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -167,10 +238,13 @@ def main():
                  "ddp": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
                  # tests/test_gpu_sequence_fuzz.py's random sequence at the defaults
                  "seq": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
-                 "seqs": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
+                 "seqs": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER),
+                 # a graph replay beside an eager launch of the same comm (launch guard)
+                 "guard": (C.FIFO_UNCACHED, C.LOCALITY_RECEIVER)}
     direct_kw = {"direct": dict(direct_bytes=8 << 20, oneshot_bytes=-1, ll_bytes=-1),
                  "oneshot": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=-1),
-                 "ll": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=1 << 20)}
+                 "ll": dict(direct_bytes=-1, oneshot_bytes=8 << 20, ll_bytes=1 << 20),
+                 "guard": dict(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=1 << 20, lanes=2, channel_count=2)}
     names = os.environ.get("IPC_MODES", "uncached,device").split(",")
     results = {}
     # processes sharing one GPU: the library's default lanes; mccsCommConnect
@@ -179,11 +253,14 @@ def main():
     lanes = None
     for mode in names:
         fifo, loc = all_modes[mode]
+        kw = dict(direct_kw.get(mode, {}))
+        kw.setdefault("lanes", lanes)
         comm = C.init_communicator_rank(rank, world, dev, exchange,
-                                        C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, lanes=lanes,
-                                                     **direct_kw.get(mode, {})))
-        if mode in ("ddp", "seq", "seqs"):
-            if mode == "ddp":
+                                        C.CommConfig(fifo_memory=fifo, locality=loc, timeout_ms=20000, **kw))
+        if mode in ("ddp", "seq", "seqs", "guard"):
+            if mode == "guard":
+                results.update(guard_overlap(comm, rank, world, orc, vnode))
+            elif mode == "ddp":
                 results.update(ddp_stream(comm, rank, world, orc, vnode))
             else:
                 results.update(seq_stream(comm, rank, world, orc, vnode, streams=mode == "seqs"))

@@ -13,9 +13,17 @@ BIN = os.path.join(HERE, "capi", "capi_allreduce")
 
 @pytest.mark.gpu
 def test_c_driver_runs():
+    """Also section 5: a stream destroyed with an
+    AllReduce still queued, a new stream at the same address, an AllReduce on
+    it at once.  Under the runtime a C / Rust caller links (ROCm 7.2, no
+    torch) the library tells streams apart by hipStreamGetId, so it orders the
+    second launch after the first on the host: both exact, and the launch
+    guard never saw them overlap."""
     assert os.path.exists(BIN), "build it with __graft_entry__.build() / python -m mccs_amd.build"
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "capi ok" in r.stdout, r.stdout + r.stderr
+    assert "stream ids: native" in r.stdout, r.stdout  # the id branch, not the address fallback
+    assert "guard waits: 0" in r.stdout, r.stdout
 
 
 def test_header_is_plain_c11():

@@ -675,3 +675,79 @@ def test_launch_larger_than_the_work_fifo_is_refused(fake, monkeypatch):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_capture_leaves_the_eager_issue_order_alone(fake):
+    """a launch captured into a graph used to overwrite the comm's
+    latest-launch record (stream, event, sync owner) although a capture
+    launches nothing; the next eager launch on a third stream then skipped
+    its wait for the eager launch before the capture.  Eager on stream A,
+    capture on stream C, eager on stream B: B must wait on A's launch."""
+    fake(2)
+    comms = C.init_all([0, 1], C.CommConfig(buffer_size=1 << 20))
+    lib = _lib.load()
+    lib.mccs_test_fake_capture.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    try:
+        def group(stream):
+            with C.group():
+                for r, c in enumerate(comms):
+                    C.all_reduce(c, 0x10000000 * (r + 1), 0x10000000 * (r + 1) + 0x8000000, 1 << 20, F32, SUM,
+                                 stream=stream)
+
+        group(0x7000)  # eager on A
+        _log()
+        assert lib.mccs_test_fake_capture(0x7200, 1) == 0
+        group(0x7200)  # captured on C
+        assert lib.mccs_test_fake_capture(0x7200, 0) == 0
+        cap = _log()
+        assert [kv["stream"] for k, kv in cap if k == "launch"] == [str(0x7200)] * 2, cap
+        assert not any(k == "stream_wait" for k, _ in cap), "a captured launch waited on an event outside its graph"
+        group(0x7100)  # eager on B: ordered after A's launch on every device
+        ev = _log()
+        waits = [kv for k, kv in ev if k == "stream_wait"]
+        assert sorted(int(kv["dev"]) for kv in waits) == [0, 1], ev
+        assert all(kv["stream"] == str(0x7100) for kv in waits), waits
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+@pytest.mark.parametrize("n", [1, 3, 8])
+def test_launches_carry_the_guard_order(fake, n):
+    """Every launch names its rank slots in the order of their launch guards'
+    addresses (launch_guard.h: fused launches take their guards in that one
+    order, so two of them can never each hold a guard the other waits for);
+    the guard line sits at MCCS_GUARD_OFF in each comm's device allocation."""
+    fake(1)
+    comms = C.init_all([0] * n, C.CommConfig(buffer_size=1 << 20))
+    try:
+        for count in (1 << 20, 1000):  # ring, then a direct-sized bucket (LL at n >= 2)
+            _log()
+            _allreduce_group(comms, count)
+            launch = [kv for k, kv in _log() if k == "launch"]
+            assert len(launch) == 1
+            order = int(launch[0]["guard_order"])
+            slots = [(order >> (4 * i)) & 15 for i in range(n)]
+            assert sorted(slots) == list(range(n))
+            devs = [c.dev_comm() for c in comms]
+            assert [devs[k] for k in slots] == sorted(devs)
+            assert launch[0]["no_guard"] == "0"
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_guard_test_hook_is_read_at_connect(fake, monkeypatch):
+    """MCCS_LAUNCH_GUARD=0 (with MCCS_TEST_HOOKS=1) turns the guard off for
+    communicators connected afterwards: the GPU test's control case."""
+    fake(1)
+    monkeypatch.setenv("MCCS_LAUNCH_GUARD", "0")
+    comms = C.init_all([0] * 2, C.CommConfig(buffer_size=1 << 20))
+    try:
+        for count in (1 << 20, 1000):
+            _log()
+            _allreduce_group(comms, count)
+            assert [kv["no_guard"] for k, kv in _log() if k == "launch"] == ["1"]
+    finally:
+        for c in comms:
+            c.destroy()

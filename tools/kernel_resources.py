@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Register, scratch and LDS use of the shipped ring kernels (gfx950).
+"""Register, scratch and LDS use of the shipped ring and direct kernels (gfx950).
 
 Compiles the ring translation units (ring.hip, ring_ar_*.hip) with
 --save-temps into a scratch directory and reads each kernel's AMDGPU
@@ -55,7 +55,7 @@ def main():
     if args[:1] == ["--diff"]:
         diff = json.load(open(args[1]))
         args = args[2:]
-    srcs = sorted(glob.glob(os.path.join(CSRC, "ring*.hip")))
+    srcs = sorted(glob.glob(os.path.join(CSRC, "ring*.hip"))) + [os.path.join(CSRC, "direct.hip")]
     with tempfile.TemporaryDirectory() as tmp, ThreadPoolExecutor(8) as ex:
         res = {}
         for r in ex.map(lambda s: compile_tu(s, args, tmp), srcs):
