@@ -446,16 +446,32 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
   bool all_uc = true, release = false;
   {
     StepScope st("handle check");
+    // A refused handle set is refused by every rank: each compares every
+    // handle with its own and with rank 0's, and any disagreement between two
+    // ranks shows up at every rank.  So no rank goes on to map this rank's
+    // arena, and it need not wait for peers' release words when it is
+    // destroyed (a service retrying failed connects lost one FIFO
+    // arena per attempt on every rank).  Failures after this point keep the
+    // wait: a peer past its own check may have mapped the arena, and its ring
+    // sender writes up to fifo_slots steps into it before any credit.
+    auto refuse = [&](const char* why) {
+      c->arena_shared = false;
+      err_note(__FILE__, __LINE__, "%s", why);
+      return mccsInvalidArgument;
+    };
     for (int r = 0; r < c->nranks; ++r) {
       const ConnectHandle& h = hs[r];
       const std::string why = handle_mismatch(c, h, hs[c->rank], r);
       // ranks disagree on the communicator profile
-      if (!why.empty()) MCCS_FAIL(mccsInvalidArgument, "%s", why.c_str());
+      if (!why.empty()) return refuse(why.c_str());
       all_uc = all_uc && h.fifo_memory != MCCS_FIFO_DEVICE;
       release = release || h.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE;
-      if (h.lanes != hs[0].lanes || h.lanes_auto != hs[0].lanes_auto)
-        MCCS_FAIL(mccsInvalidArgument, "rank %d's lanes %d (auto %d) differ from rank 0's %d (auto %d)", r, h.lanes,
-                  h.lanes_auto, hs[0].lanes, hs[0].lanes_auto);
+      if (h.lanes != hs[0].lanes || h.lanes_auto != hs[0].lanes_auto) {
+        char b[160];
+        std::snprintf(b, sizeof(b), "rank %d's lanes %d (auto %d) differ from rank 0's %d (auto %d)", r, h.lanes,
+                      h.lanes_auto, hs[0].lanes, hs[0].lanes_auto);
+        return refuse(b);
+      }
     }
   }
   // Ranks of this communicator that share a GPU as separate processes run

@@ -11,6 +11,7 @@
 // peer access (same process) or IPC (one rank per process).
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -587,6 +588,24 @@ mccsResult_t comm_stream(Comm* c, hipStream_t* out) {
 // whose launches this comm's event tracked read it through sync_owner at wait
 // time, so they see the new one; the old one is destroyed once no thread
 // synchronizes on it.
+// Waits until no thread synchronizes on the comm's event outside the
+// live-comm lock (comm_wait_last_launch).  Such a wait can last as long as a
+// kernel spinning on late peers (up to the watchdog, 10 min by default), so
+// after a few yields this sleeps, backing off to 1 ms (a busy
+// spin here burnt a core for that long).
+static void wait_no_waiters(Comm* c) {
+  long ns = 0;
+  for (int i = 0; c->waiters.load() > 0; ++i) {
+    if (i < 64) {
+      sched_yield();
+      continue;
+    }
+    ns = ns ? std::min(ns * 2, 1000000L) : 1000L;
+    const timespec ts{0, ns};
+    nanosleep(&ts, nullptr);
+  }
+}
+
 mccsResult_t comm_make_event_ipc(Comm* c) {
   if (c->event_ipc) return mccsSuccess;
   StepScope st("interprocess comm event");
@@ -601,7 +620,7 @@ mccsResult_t comm_make_event_ipc(Comm* c) {
     old = c->event;
     c->event = e;
   }
-  while (c->waiters.load() > 0) sched_yield();
+  wait_no_waiters(c);
   (void)rt().EventDestroy(old);
   c->event_ipc = true;
   return mccsSuccess;
@@ -648,7 +667,7 @@ mccsResult_t comm_free(Comm* c) {
     for (Comm* x : g_live_comms)
       if (x->sync_owner == c) x->sync_owner = nullptr;
   }
-  while (c->waiters.load() > 0) sched_yield();  // a fused comm's wait on our event
+  wait_no_waiters(c);  // a fused comm's wait on our event
   if (c->stream) (void)rt().StreamSynchronize(c->stream);
   // Our kernels are done: release every peer's arena (its release word for
   // our rank gets its tenancy's epoch), then unmap it.  Best effort: a peer

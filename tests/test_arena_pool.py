@@ -124,3 +124,43 @@ def test_arena_waits_for_every_peer_release(lib):
     for cs in again:
         for c in cs:
             c.destroy()
+
+
+def test_refused_connect_does_not_strand_the_arena(lib):
+    """an arena is marked shared when SetupRank exports it, so its
+    destroy pools it until every peer writes its release word -- but a peer
+    writes that word only if its Connect mapped the arena.  A handle set the
+    ranks refuse is refused by every rank before any IPC open, so those arenas
+    go back to the pool free (a service retrying failed connects used to lose
+    one arena per attempt on every rank)."""
+    from test_rank_per_process import PID_OFFSET
+
+    n = 2
+    hsize = lib.mccsConnectHandleSize()
+    hs, bufs = [], []
+    for r in range(n):
+        buf = (ctypes.c_char * hsize)()
+        h = ctypes.c_void_p()
+        cfg, keep = C.CommConfig().to_c(n)
+        assert lib.mccsCommSetupRank(ctypes.byref(h), r, n, r, ctypes.byref(cfg), buf) == 0
+        del keep
+        hs.append(h)
+        bufs.append(bytearray(buf))
+    bufs[1][0:4] = (0x12345678).to_bytes(4, "little")  # rank 1's handle is not a connect handle
+    for r in range(n):
+        mine = []
+        for q in range(n):
+            b = bytearray(bufs[q])
+            if q != r:
+                b[PID_OFFSET:PID_OFFSET + 4] = (0x7ffffff0 - q).to_bytes(4, "little")
+            mine.append(bytes(b))
+        allh = ctypes.create_string_buffer(b"".join(mine), hsize * n)
+        assert lib.mccsCommConnect(hs[r], allh) == 4  # mccsInvalidArgument, on every rank
+    for h in hs:
+        assert lib.mccsCommDestroy(h) == 0
+    assert lib.mccs_test_pool_waiting() == 0
+    _calls(lib)
+    again = C.init_all([0, 1])
+    assert _calls(lib).count("MallocUncached") == 0  # both arenas were reusable at once
+    for c in again:
+        c.destroy()
