@@ -22,6 +22,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
 
 #include "comm.h"
 #include "dtypes.h"
@@ -400,28 +401,34 @@ static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
 // Blocks of the fused multi-rank kernels the device holds at once, minimised
 // over every (func, dtype, op) instantiation.  Ranks sharing a GPU spin on
 // each other's flags, so their fused launch must be fully co-resident.
+// A probe the runtime refuses returns 0 ("unknown": callers check it) and
+// is not cached, so a transient failure does not stick for the process; the
+// cache is per device runtime (rt_generation: the real one, or a test fake).
 int coresident_ring_blocks(int block, int device) {
   static std::mutex mu;
-  static std::map<std::pair<int, int>, int> cache;  // (device, block) -> blocks
+  static std::map<std::tuple<unsigned, int, int>, int> cache;  // (runtime, device, block) -> blocks
+  const auto key = std::make_tuple(rt_generation(), device, block);
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find({device, block});
+    auto it = cache.find(key);
     if (it != cache.end()) return it->second;
   }
   DeviceGuard g(device);
   int ncu = 0;
   if (rt().CuCount(&ncu, device) != hipSuccess) return 0;
   int best = 1 << 30;
-  auto probe = [&](const void* fn) {
-    int per_cu = 0;
-    if (!fn || rt().BlocksPerCu(&per_cu, fn, block) != hipSuccess) per_cu = 0;
-    best = std::min(best, per_cu);
-  };
-  probe(ring_multi_kernel_ptr(mccsFuncAllGather, mccsInt8, 0));
+  const void* fns[1 + mccsNumTypes * 4];
+  int nf = 0;
+  fns[nf++] = ring_multi_kernel_ptr(mccsFuncAllGather, mccsInt8, 0);
   for (int dt = 0; dt < mccsNumTypes; ++dt)
-    for (int op = 0; op < 4; ++op) probe(ring_multi_kernel_ptr(mccsFuncAllReduce, dt, op));
+    for (int op = 0; op < 4; ++op) fns[nf++] = ring_multi_kernel_ptr(mccsFuncAllReduce, dt, op);
+  for (int i = 0; i < nf; ++i) {
+    int per_cu = 0;
+    if (!fns[i] || rt().BlocksPerCu(&per_cu, fns[i], block) != hipSuccess) return 0;
+    best = std::min(best, per_cu);
+  }
   std::lock_guard<std::mutex> lk(mu);
-  return cache[{device, block}] = best * ncu;
+  return cache[key] = best * ncu;
 }
 
 // Workgroups of the direct kernels the device holds at once (min over the
@@ -429,10 +436,11 @@ int coresident_ring_blocks(int block, int device) {
 // workgroups, and those of ranks sharing the GPU, must be resident together.
 static int coresident_direct_blocks(int device, int* ncu_out = nullptr) {
   static std::mutex mu;
-  static std::map<int, std::pair<int, int>> cache;  // device -> (blocks, CUs)
+  static std::map<std::pair<unsigned, int>, std::pair<int, int>> cache;  // (runtime, device) -> (blocks, CUs)
+  const auto key = std::make_pair(rt_generation(), device);
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find(device);
+    auto it = cache.find(key);
     if (it != cache.end()) {
       if (ncu_out) *ncu_out = it->second.second;
       return it->second.first;
@@ -446,11 +454,11 @@ static int coresident_direct_blocks(int device, int* ncu_out = nullptr) {
     for (int op = 0; op < 4; ++op) {
       int per_cu = 0;
       const void* fn = direct_kernel_ptr(dt, op);
-      if (!fn || rt().BlocksPerCu(&per_cu, fn, MCCS_DIRECT_THREADS) != hipSuccess) per_cu = 0;
+      if (!fn || rt().BlocksPerCu(&per_cu, fn, MCCS_DIRECT_THREADS) != hipSuccess) return 0;  // not cached
       best = std::min(best, per_cu);
     }
   std::lock_guard<std::mutex> lk(mu);
-  cache[device] = {best * ncu, ncu};
+  cache[key] = {best * ncu, ncu};
   if (ncu_out) *ncu_out = ncu;
   return best * ncu;
 }

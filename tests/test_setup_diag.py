@@ -123,7 +123,9 @@ def test_every_setup_call_failure_is_named(lib):
         _fresh(lib)
         lib.mccs_test_fake_fail(name.encode(), k, OOM)
         rc, h, handle, err, herr = _setup(lib)
-        if (name, k) in ABSORBED:
+        # every residency probe is absorbed: a refused one reads as "unknown"
+        # (0, checked where it is used) and is not cached
+        if (name, k) in ABSORBED or name == "BlocksPerCu":
             assert rc == 0, (name, k, err)
             lib.mccsCommDestroy(h)
             continue
