@@ -135,7 +135,7 @@ __device__ __forceinline__ void direct_pieces(const DirectWalk& w, const uint8_t
 
 struct DirectShm {
   uint8_t idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];  // a.idx2rank (walk lookups stay in LDS)
-  char* region[MCCS_DIRECT_MAX_RANKS];                          // me.region
+  char* region[MCCS_DIRECT_MAX_RANKS];                          // a.region
   uint64_t seq;
   uint64_t e_in;                            // E_IN at launch start
   uint64_t e_self;                          // E_SELF at launch start
@@ -275,7 +275,7 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
   __shared__ DirectShm sh;
   const mccsDirectRank& me = a.r[blockIdx.y];
   const int n = (int)a.nranks;
-  char* const mine = me.region[me.rank];
+  char* const mine = a.region[me.rank];
   volatile uint32_t* abortFlag = me.abort_flag;
   mccsRingKernelCfg ecfg{};
   ecfg.err_line = me.err_line;
@@ -307,7 +307,7 @@ __device__ __forceinline__ void direct_body(const mccsDirectArgs& a) {
     if (lane < MCCS_DIRECT_MAX_RANKS) {
       sh.owned[lane] = a.owned[lane];
       sh.sent[lane] = 0;
-      sh.region[lane] = me.region[lane];
+      sh.region[lane] = a.region[lane];
     }
     // the walk's table, 4 bytes per lane
     ((uint32_t*)sh.idx2rank)[lane] = ((const uint32_t*)a.idx2rank)[lane];
@@ -568,7 +568,7 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
   __shared__ uint8_t s_idx2rank[MCCS_MAX_NCHANNELS][MCCS_DIRECT_MAX_RANKS];
   const mccsDirectRank& me = a.r[blockIdx.y];
   const uint32_t n = a.nranks, rank = me.rank;
-  char* const mine = me.region[rank];
+  char* const mine = a.region[rank];
   volatile uint32_t* abortFlag = me.abort_flag;
   mccsRingKernelCfg ecfg{};
   ecfg.err_line = me.err_line;
@@ -619,7 +619,7 @@ __device__ __forceinline__ void direct_ll_body(const mccsDirectArgs& a) {
 #pragma unroll
       for (uint32_t t = 0; t < MCCS_DIRECT_MAX_RANKS; ++t)
         if (t < n && t != rank) {
-          uint64_t* p = (uint64_t*)(me.region[t] + llbase + (int64_t)rank * lslot + (int64_t)wd * 16);
+          uint64_t* p = (uint64_t*)(a.region[t] + llbase + (int64_t)rank * lslot + (int64_t)wd * 16);
           __hip_atomic_store(p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }

@@ -649,6 +649,13 @@ hipError_t comm_wait_last_launch(Comm* c) {
   return rt().DeviceSynchronize();  // nothing recorded the launch: every stream of the device
 }
 
+hipError_t comm_query_last_launch(Comm* c) {
+  if (c->event_recorded) return rt().EventQuery(c->event);
+  std::lock_guard<std::mutex> lk(g_live_mu);  // the owner's event: read while it cannot be replaced or freed
+  if (c->sync_owner && g_live_comms.count(c->sync_owner)) return rt().EventQuery(c->sync_owner->event);
+  return hipErrorNotReady;  // nothing recorded the launch: it cannot be told finished
+}
+
 hipError_t comm_order_after_last_launch(Comm* c, hipStream_t s) {
   if (c->event_recorded) return rt().StreamWaitEvent(s, c->event);
   std::lock_guard<std::mutex> lk(g_live_mu);  // the owner's event: read while it cannot be replaced or freed

@@ -158,10 +158,23 @@ struct WorkElemHost {
   uint8_t bid, nChannels;
 };
 
+// One KernelWork (plan.rs): up to MCCS_MAX_WORK_ELEMENTS elements of one
+// function, held inline so planning a launch allocates nothing.
+struct HostWork {
+  WorkElemHost e[MCCS_MAX_WORK_ELEMENTS];
+  int n = 0;
+  int func = 0;  // func id (for batching)
+  size_t size() const { return (size_t)n; }
+  const WorkElemHost& operator[](size_t i) const { return e[i]; }
+};
+
 struct ChannelSchedule {  // plan.rs ChanWorkSchedule
   size_t coll_bytes = 0;
-  std::vector<std::vector<WorkElemHost>> works;  // KernelWork list
-  std::vector<int> work_func;                   // func id per work (for batching)
+  std::vector<HostWork> works;  // KernelWork list
+  void reset() {                // after a launch: empty, capacity kept for the next
+    coll_bytes = 0;
+    works.clear();
+  }
 };
 
 // Entries of a comm's graph work arena held by captured launches.  A
@@ -279,6 +292,11 @@ struct Comm {
     size_t count;
   } direct{};
   int share = 1;         // ranks of this communicator on this rank's GPU (co-residency of spinning launches)
+  // operator / test overrides read once at creation (make_comm), not per
+  // launch: MCCS_INLINE_WORKS=0 (works always through the work FIFO) and
+  // MCCS_DIRECT_BLOCKS (most workgroups per rank of a direct launch)
+  bool inline_works = true;
+  int direct_blocks = 128;
   // Every device of the communicator can perform atomics on every other's
   // memory (the direct kernel's hand-off counts are remote atomics); all ranks
   // derive it from the same device set, so they agree.
@@ -301,6 +319,9 @@ mccsResult_t comm_build_device(Comm* c);
 void default_rings(int nranks, int nch_req, std::vector<std::vector<int>>* rings);
 mccsResult_t comm_free(Comm* c);
 hipError_t comm_wait_last_launch(Comm* c);  // host wait for the comm's latest launch
+// hipSuccess once the comm's latest launch finished (its event, or its fused
+// launch owner's); hipErrorNotReady while it runs or when nothing recorded it.
+hipError_t comm_query_last_launch(Comm* c);
 // Makes stream `s` wait for the comm's latest launch (none recorded: no-op).
 hipError_t comm_order_after_last_launch(Comm* c, hipStream_t s);
 mccsResult_t comm_set_kernel_cfg(Comm* c);

@@ -49,27 +49,32 @@ void task_schema(size_t total_bytes, int nch_cfg, int* nch_out, int* nthreads_ou
 static inline bool rolling_less_u32(uint32_t a, uint32_t b) { return (uint32_t)(a - b) > 0x7fffffffu; }
 static inline uint32_t rolling_min_u32(uint32_t a, uint32_t b) { return (uint32_t)(b - a) <= 0x7fffffffu ? a : b; }
 
-// k least-loaded channels, ties by id (ChannelLoad ordering, plan.rs:673-692)
-static std::vector<int> select_channels(const Comm* c, int k) {
-  std::vector<int> ids(c->nch);
-  for (int i = 0; i < c->nch; ++i) ids[i] = i;
-  std::stable_sort(ids.begin(), ids.end(),
-                   [&](int a, int b) { return c->sched[a].coll_bytes < c->sched[b].coll_bytes; });
-  ids.resize(std::min(k, c->nch));
-  return ids;
+// The k least-loaded channels, ties by id (ChannelLoad ordering,
+// plan.rs:673-692), into ids[0..return); no allocation.
+static int select_channels(const Comm* c, int k, int* ids) {
+  int n = 0;
+  for (int i = 0; i < c->nch; ++i) {  // stable insertion sort by load
+    int j = n++;
+    for (; j > 0 && c->sched[ids[j - 1]].coll_bytes > c->sched[i].coll_bytes; --j) ids[j] = ids[j - 1];
+    ids[j] = i;
+  }
+  return std::min(k, c->nch);
 }
 
 static void enqueue_elem(ChannelSchedule& s, const WorkElemHost& e, int func_index, size_t esize) {
   s.coll_bytes += e.count * esize;
   if (!s.works.empty()) {
-    auto& tail = s.works.back();
-    if (s.work_func.back() == func_index && tail[0].nWarps == e.nWarps && (int)tail.size() < kMaxElemsPerWork) {
-      tail.push_back(e);
+    HostWork& tail = s.works.back();
+    if (tail.func == func_index && tail.e[0].nWarps == e.nWarps && tail.n < kMaxElemsPerWork) {
+      tail.e[tail.n++] = e;
       return;
     }
   }
-  s.works.push_back({e});
-  s.work_func.push_back(func_index);
+  s.works.emplace_back();
+  HostWork& w = s.works.back();
+  w.e[0] = e;
+  w.n = 1;
+  w.func = func_index;
 }
 
 static mccsResult_t ring_enqueue(Comm* c, int func, int dtype, int op, const void* send, void* recv, size_t count) {
@@ -77,15 +82,16 @@ static mccsResult_t ring_enqueue(Comm* c, int func, int dtype, int op, const voi
   const size_t total = func == mccsFuncAllGather ? count * c->nranks : count * esize;  // task.rs:95-102
   int nch = 0, nthr = 0;
   task_schema(total, c->nch, &nch, &nthr);
-  const std::vector<int> chans = select_channels(c, nch);
-  for (int bid = 0; bid < (int)chans.size(); ++bid) {
+  int chans[MCCS_MAX_NCHANNELS];
+  const int nsel = select_channels(c, nch, chans);
+  for (int bid = 0; bid < nsel; ++bid) {
     WorkElemHost e{};
     e.nWarps = (uint8_t)(nthr / WARP_SIZE);
     e.send = send;
     e.recv = recv;
     e.count = count;
     e.bid = (uint8_t)bid;
-    e.nChannels = (uint8_t)chans.size();
+    e.nChannels = (uint8_t)nsel;
     enqueue_elem(c->sched[chans[bid]], e, /*funcIndex, unused (plan.rs:585)*/ 0,
                  func == mccsFuncAllGather ? 1 : esize);
   }
@@ -97,7 +103,7 @@ static mccsResult_t ring_enqueue(Comm* c, int func, int dtype, int op, const voi
 }
 
 void plan_discard(Comm* c) {
-  for (auto& s : c->sched) s = ChannelSchedule{};
+  for (auto& s : c->sched) s.reset();
   c->plan_pending = false;
   c->plan_direct = false;
 }
@@ -149,7 +155,7 @@ mccsResult_t plan_enqueue(Comm* c, int func, int dtype, int op, const void* send
   return ring_enqueue(c, func, dtype, op, send, recv, count);
 }
 
-static mccsDevWork to_dev_work(const std::vector<WorkElemHost>& elems, bool in_fifo, bool is_last, uint32_t u) {
+static mccsDevWork to_dev_work(const HostWork& elems, bool in_fifo, bool is_last, uint32_t u) {
   mccsDevWork w;
   std::memset(&w, 0, sizeof(w));
   for (size_t i = 0; i < elems.size(); ++i) {
@@ -185,7 +191,7 @@ static mccsResult_t wait_work_queue(Comm* c, uint32_t target) {
       if (ackd[ch] == c->chan_next[ch]) __atomic_store_n(&c->h_done[ch], all, __ATOMIC_RELAXED);
     c->work_acked_min = all;
     if (!rolling_less_u32(c->work_acked_min + c->work_depth, target)) return mccsSuccess;
-    if ((spins & 0xfffff) == 0xfffff && rt().EventQuery(c->event) == hipSuccess) {
+    if ((spins & 0xfffff) == 0xfffff && comm_query_last_launch(c) == hipSuccess) {
       // stream idle but acks missing: the kernel aborted
       MCCS_FAIL(mccsRemoteError, "work FIFO full and its kernel no longer running (aborted or timed out)");
     }
@@ -216,11 +222,15 @@ static bool eager_events() {
 // 4 bits each (launch_guard.h: every fused launch takes its guards in this
 // one order, so two of them never hold each other's).
 static uint64_t guard_order(const std::vector<Comm*>& comms, const std::vector<int>& idx) {
-  std::vector<int> k(idx.size());
-  for (size_t i = 0; i < k.size(); ++i) k[i] = (int)i;
-  std::sort(k.begin(), k.end(), [&](int a, int b) { return comms[idx[a]]->d_guard < comms[idx[b]]->d_guard; });
+  int k[MCCS_MULTI_MAX_RANKS];
+  const int n = (int)idx.size();
+  for (int i = 0; i < n; ++i) {  // insertion sort of the slots by guard address
+    int j = i;
+    for (; j > 0 && comms[idx[k[j - 1]]]->d_guard > comms[idx[i]]->d_guard; --j) k[j] = k[j - 1];
+    k[j] = i;
+  }
   uint64_t order = 0;
-  for (size_t i = 0; i < k.size(); ++i) order |= (uint64_t)k[i] << (4 * i);
+  for (int i = 0; i < n; ++i) order |= (uint64_t)k[i] << (4 * i);
   return order;
 }
 
@@ -284,7 +294,7 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld, hipGraph_t graph)
   ld->work = c->d_graph_work + start;
   ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
   ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
-  for (auto& s : c->sched) s = ChannelSchedule{};
+  for (auto& s : c->sched) s.reset();
   c->plan_pending = false;
   return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
 }
@@ -295,8 +305,7 @@ static mccsResult_t upload_work_graph(Comm* c, LaunchDesc* ld, hipGraph_t graph)
 // channels used per rank (0: use the work FIFO).  MCCS_INLINE_WORKS=0 turns it
 // off.
 static int inline_channels(const Comm* c) {
-  const char* v = std::getenv("MCCS_INLINE_WORKS");  // read per launch: tests switch it
-  if (v && std::atoi(v) == 0) return 0;
+  if (!c->inline_works) return 0;
   int used = 0;
   for (int ch = 0; ch < c->nch; ++ch) {
     const auto& works = c->sched[ch].works;
@@ -323,7 +332,7 @@ static mccsResult_t upload_work_inline(Comm* c, LaunchDesc* ld, mccsMultiLaunchA
   ld->work_inline = true;
   ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
   ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
-  for (auto& s : c->sched) s = ChannelSchedule{};
+  for (auto& s : c->sched) s.reset();
   c->plan_pending = false;
   return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
 }
@@ -393,7 +402,7 @@ static mccsResult_t upload_work(Comm* c, LaunchDesc* ld) {
   ld->work = c->d_work + (first & qmask);
   ld->fn = ring_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
   ld->multi_fn = ring_multi_kernel_ptr(c->plan_func, c->plan_dtype, c->plan_op);
-  for (auto& s : c->sched) s = ChannelSchedule{};
+  for (auto& s : c->sched) s.reset();
   c->plan_pending = false;
   return (ld->fn && ld->multi_fn) ? mccsSuccess : mccsInvalidArgument;
 }
@@ -463,14 +472,6 @@ static int coresident_direct_blocks(int device, int* ncu_out = nullptr) {
   return best * ncu;
 }
 
-// MCCS_DIRECT_BLOCKS: most workgroups per rank of a direct launch (default
-// 128; read per launch: sweeps switch it).
-static int direct_max_blocks() {
-  const char* e = std::getenv("MCCS_DIRECT_BLOCKS");
-  const int x = e ? std::atoi(e) : 0;
-  return x > 0 ? x : 128;
-}
-
 // Every comm of the device group holds one direct AllReduce of the same shape
 // (fused ranks share the launch's walk arguments).
 static bool direct_group(std::vector<Comm*>& comms, const std::vector<int>& idx) {
@@ -484,7 +485,7 @@ static bool direct_group(std::vector<Comm*>& comms, const std::vector<int>& idx)
         ck->layout.direct_slot != c0->layout.direct_slot || ck->layout.oneshot_slot != c0->layout.oneshot_slot ||
         ck->layout.ll_slot != c0->layout.ll_slot || ck->cfg.ll_bytes != c0->cfg.ll_bytes ||
         ck->cfg.oneshot_bytes != c0->cfg.oneshot_bytes || ck->cfg.direct_bytes != c0->cfg.direct_bytes ||
-        ck->nch != c0->nch)
+        ck->nch != c0->nch || ck->peer_arena != c0->peer_arena)  // one region table for every slot
       return false;
   }
   return idx.size() <= MCCS_MULTI_MAX_RANKS;
@@ -501,7 +502,8 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
   const size_t esize = gather ? 1 : (size_t)elem_bytes(c0->plan_dtype);
   int nch = 0, nthr = 0;
   task_schema(c0->direct.count * esize, c0->nch, &nch, &nthr);
-  const std::vector<int> chans = select_channels(c0, nch);
+  int chans[MCCS_MAX_NCHANNELS];
+  const int nsel = select_channels(c0, nch, chans);
   std::memset(da, 0, sizeof(*da));
   const int n = c0->nranks;
   da->count = c0->direct.count;
@@ -518,12 +520,12 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
              : oneshot ? MCCS_DIRECT_ONE_SHOT
                        : MCCS_DIRECT_TWO_SHOT;
   da->nranks = (uint32_t)n;
-  da->nch = (uint32_t)chans.size();
+  da->nch = (uint32_t)nsel;
   da->nthr_ref = (uint32_t)nthr;
   da->buff_size = (uint32_t)c0->cfg.buffer_size;
   da->fence_mode = c0->kcfg.fence_mode;
   da->timeout_ticks = c0->kcfg.timeout_ticks;
-  for (size_t bid = 0; bid < chans.size(); ++bid) {
+  for (int bid = 0; bid < nsel; ++bid) {
     const std::vector<int>& ring = c0->rings[chans[bid]];
     const int pos0 = (int)(std::find(ring.begin(), ring.end(), 0) - ring.begin());
     for (int k = 0; k < n; ++k) da->idx2rank[bid][k] = (uint8_t)ring[(pos0 + k) % n];
@@ -550,7 +552,8 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
     r.recv = ck->direct.recv;
     for (int t = 0; t < n; ++t) {
       if (!ck->peer_arena[t]) return mccsInternalError;
-      r.region[t] = ck->peer_arena[t] + ck->layout.direct_off();
+      if (k == 0) da->region[t] = ck->peer_arena[t] + ck->layout.direct_off();
+      else if (da->region[t] != ck->peer_arena[t] + ck->layout.direct_off()) return mccsInternalError;  // direct_group
     }
     r.comm = (mccsDevComm*)ck->d_comm;
     r.abort_flag = ck->d_abort;
@@ -586,9 +589,9 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
     const long x = v ? std::atol(v) : 0;
     return x >= 1024 ? x : 4096L;
   }();
-  long g = std::min<long>((long)((scatter + wg_bytes - 1) / wg_bytes), direct_max_blocks());
+  long g = std::min<long>((long)((scatter + wg_bytes - 1) / wg_bytes), c0->direct_blocks);
   // LL: one 8-byte word per thread
-  if (ll) g = std::min<long>((long)((nbytes + 8 * MCCS_DIRECT_THREADS - 1) / (8 * MCCS_DIRECT_THREADS)), direct_max_blocks());
+  if (ll) g = std::min<long>((long)((nbytes + 8 * MCCS_DIRECT_THREADS - 1) / (8 * MCCS_DIRECT_THREADS)), c0->direct_blocks);
   if (idx.size() > 1) g = std::min<long>(g, std::min(cap, ncu) / (long)idx.size());  // one fused launch
   else if (c0->share > 1) g = std::min<long>(g, std::min(cap / 2, ncu) / c0->share);  // separate processes
   g = std::max<long>(g, 1);
@@ -621,23 +624,34 @@ static mccsResult_t build_direct(std::vector<Comm*>& comms, const std::vector<in
 // hold one direct-sized AllReduce runs the direct kernel, anything else the
 // ring.
 mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_t>& user_streams) {
-  std::map<int, std::vector<int>> by_dev;
-  for (int i = 0; i < (int)comms.size(); ++i)
-    if (comms[i]->plan_pending) by_dev[comms[i]->device].push_back(i);
-  for (auto& kv : by_dev) {
-    const std::vector<int>& idx = kv.second;
-    DeviceGuard g(kv.first);
+  // pending comms grouped by device, in device order (buffers kept per
+  // thread: an eager launch allocates nothing)
+  static thread_local std::vector<int> order, idx;
+  order.clear();
+  for (int i = 0; i < (int)comms.size(); ++i) {
+    if (!comms[i]->plan_pending) continue;
+    order.push_back(i);
+    for (size_t j = order.size() - 1; j > 0 && comms[order[j - 1]]->device > comms[i]->device; --j)
+      std::swap(order[j], order[j - 1]);
+  }
+  for (size_t run = 0; run < order.size();) {
+    const int dev = comms[order[run]]->device;
+    idx.clear();
+    while (run < order.size() && comms[order[run]]->device == dev) idx.push_back(order[run++]);
+    if (idx.size() > MCCS_MULTI_MAX_RANKS)
+      MCCS_FAIL(mccsInvalidUsage, "%zu ranks share one device (at most %d)", idx.size(), (int)MCCS_MULTI_MAX_RANKS);
+    DeviceGuard g(dev);
     const bool direct = direct_group(comms, idx);
     if (!direct)
       for (int i : idx) MCCS_CHECK(demote_direct(comms[i]));
     if (!direct && idx.size() > 1) {  // checked before any work is uploaded, so the comms stay usable
       const Comm* c0 = comms[idx[0]];
-      const int cap = coresident_ring_blocks(c0->block_threads, kv.first);
+      const int cap = coresident_ring_blocks(c0->block_threads, dev);
       const long need = (long)c0->nch * c0->lanes * (long)idx.size();
       if (need > cap) {
         // would deadlock: every block spins on a peer's flag
         MCCS_FAIL(mccsInvalidUsage, "fused launch of %zu ranks x %d blocks exceeds the %d co-resident blocks of device %d",
-                  idx.size(), c0->nch * c0->lanes, cap, kv.first);
+                  idx.size(), c0->nch * c0->lanes, cap, dev);
       }
     }
     // A capturing stream records this launch into a HIP graph: its work
@@ -646,13 +660,12 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     hipGraph_t graph = nullptr;
     MCCS_HIP(rt().StreamIsCapturing(user_streams[idx[0]], &capturing));
     if (capturing) MCCS_HIP(rt().CaptureGraph(user_streams[idx[0]], &graph));
-    std::vector<LaunchDesc> lds(idx.size());
+    LaunchDesc lds[MCCS_MULTI_MAX_RANKS];
     mccsMultiLaunchArgs ma;
     mccsDirectArgs da;
     const void* fn = nullptr;
     void* args[1] = {nullptr};
     unsigned grid = 0, block = 0;
-    bool work_inline = true;  // no work-FIFO entries to acknowledge
     Comm* c0 = comms[idx[0]];
     if (direct) {
       MCCS_CHECK(build_direct(comms, idx, &da, &grid));
@@ -677,8 +690,6 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       // Communicator launches carry their hand-off policy in the arguments
       // (one launch per device; blockIdx.y = rank slot when ranks share it).
       // Fused ranks take the safest policy of the group.
-      if (idx.size() > MCCS_MULTI_MAX_RANKS)
-        MCCS_FAIL(mccsInvalidUsage, "%zu ranks share one device (at most %d)", idx.size(), (int)MCCS_MULTI_MAX_RANKS);
       ma.channelMask = lds[0].mask;
       ma.cfg = c0->kcfg;
       for (size_t k = 0; k < idx.size(); ++k) {
@@ -704,7 +715,6 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
       grid = (unsigned)(lds[0].nch_used * c0->lanes);
       block = (unsigned)c0->block_threads;
       args[0] = &ma;
-      work_inline = lds[0].work_inline;
     }
     const bool bridge = c0->cfg.bridge_streams >= 0;
     hipStream_t st = user_streams[idx[0]];
@@ -749,9 +759,12 @@ mccsResult_t plan_launch_group(std::vector<Comm*>& comms, std::vector<hipStream_
     if (stop_on_launch) MCCS_HIP(rt().LaunchKernelExt(fn, g3, dim3(block), args, st, c0->event));
     else MCCS_HIP(rt().LaunchKernel(fn, g3, dim3(block), args, st));
     // Other events are recorded only when consumed (Comm::event_recorded):
-    // cross-stream ordering, an exported backend event, or a work-FIFO launch
-    // (wait_work_queue queries the event to tell a stuck kernel from a slow one).
-    bool record = events || !work_inline || eager_events();
+    // cross-stream ordering or an exported backend event.  Fused rank slots
+    // otherwise answer for their launch through the launching comm's stop
+    // event (sync_owner): mccsCommSync waits on it and wait_work_queue asks it
+    // whether a work-FIFO kernel still runs.  (A record per fused slot was a
+    // marker packet and ~1.5 us of host time per FIFO launch.)
+    bool record = events || eager_events();
     for (size_t k = 0; k < idx.size() && !record; ++k) record = comms[idx[k]]->event_ipc;
     if (record && !stop_on_launch) MCCS_HIP(rt().EventRecord(c0->event, st));
     if (events) {

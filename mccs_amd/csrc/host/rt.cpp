@@ -297,6 +297,7 @@ class FakeRuntime final : public DeviceRuntime {
   }
   hipError_t EventRecord(hipEvent_t e, hipStream_t s) override {
     if (hipError_t r = inj("EventRecord")) return r;
+    if (quiet_) return hipSuccess;
     note("record dev=" + std::to_string(cur_) + " event=" + std::to_string((uintptr_t)e) + " stream=" + sid(s));
     return hipSuccess;
   }
@@ -320,6 +321,7 @@ class FakeRuntime final : public DeviceRuntime {
   }
   hipError_t StreamWaitEvent(hipStream_t s, hipEvent_t e) override {
     if (hipError_t r = inj("StreamWaitEvent")) return r;
+    if (quiet_) return hipSuccess;
     note("stream_wait dev=" + std::to_string(cur_) + " stream=" + sid(s) + " event=" +
          std::to_string((uintptr_t)e) + " event_dev=" + std::to_string(event_dev(e)));
     return hipSuccess;
@@ -384,6 +386,10 @@ class FakeRuntime final : public DeviceRuntime {
   }
   hipError_t LaunchKernel(const void* fn, dim3 grid, dim3 block, void** args, hipStream_t s) override {
     if (hipError_t e = inj("LaunchKernel")) return e;
+    if (quiet_) {
+      ack_fifo_works(fn, grid, args);
+      return hipSuccess;
+    }
     // every communicator of a fused ring launch must live on the launching device
     bool on_dev = true;
     unsigned inl = 0;
@@ -421,6 +427,28 @@ class FakeRuntime final : public DeviceRuntime {
          " inline_works=" + std::to_string(inl) + " stop_event=" + std::to_string((uintptr_t)stop_) +
          " kind=" + (direct ? "direct" : "ring") + extra);
     return hipSuccess;
+  }
+  // Quiet fake: what a ring kernel reading its works from the work FIFO
+  // does to the host (common.h:153-155): each channel's last work stores its
+  // doneAcks, so a loop of FIFO launches does not fill the FIFO.
+  void ack_fifo_works(const void* fn, dim3 grid, void** args) {
+    if (!fn || !args || grid.y < 1 || grid.y > MCCS_MULTI_MAX_RANKS) return;
+    for (int dt = 0; dt < mccsNumTypes; ++dt)
+      for (int op = 0; op < 4; ++op)
+        if (fn == direct_kernel_ptr(dt, op)) return;
+    const mccsMultiLaunchArgs* ma = (const mccsMultiLaunchArgs*)args[0];
+    if (ma->inline_works) return;
+    const int nch = __builtin_popcountll(ma->channelMask);
+    for (unsigned k = 0; k < grid.y; ++k) {
+      const mccsDevCommAndChannels* cc = (const mccsDevCommAndChannels*)ma->comm[k];
+      uint64_t m = ma->channelMask;
+      for (int i = 0; i < nch; ++i, m &= m - 1) {
+        const int ch = __builtin_ctzll(m);
+        const mccsDevWork* w = ma->work[k] + i;
+        while (!w->header.isLast) w = ma->work[k] + w->header.workNext;
+        if (w->header.inFifo) *cc->channels[ch].workFifoDone = w->header.doneAcks;
+      }
+    }
   }
   hipError_t BlocksPerCu(int* per_cu, const void*, int) override {
     *per_cu = 1;
@@ -488,6 +516,7 @@ class FakeRuntime final : public DeviceRuntime {
   // threads' calls go on meanwhile), and returns the armed error for it, if
   // this is the one.
   hipError_t inj(const char* name) {
+    if (quiet_) return hipSuccess;
     int delay = 0;
     hipError_t e = hipSuccess;
     {
@@ -533,9 +562,15 @@ class FakeRuntime final : public DeviceRuntime {
   }
   static std::string sid(hipStream_t s) { return std::to_string((uintptr_t)s); }
   void note(const std::string& line) {
+    if (quiet_) return;
     std::lock_guard<std::mutex> lk(mu_);
     log_ << line << '\n';
   }
+
+ public:
+  std::atomic<bool> quiet_{false};  // no event log (host-cost measurements of the library itself)
+
+ private:
   int ndev_, cur_ = 0;
   hipEvent_t stop_ = nullptr;  // the stop event of the launch being logged (LaunchKernelExt)
   uintptr_t next_id_ = 0;
@@ -671,6 +706,17 @@ extern "C" int mccs_test_fake_recreate_stream(void* stream) {
   mccs::FakeRuntime* f = mccs::g_fake.load();
   if (!f) return -1;
   f->recreate_stream((hipStream_t)stream);
+  return 0;
+}
+
+// Quiet fake (1): no event log, no call trace, no injected failures or
+// delays, so a loop of collectives on it times the library's own host path
+// (tools/host_overhead.c --fake).  -1 without a fake.
+extern "C" int mccs_test_fake_quiet(int quiet) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  f->quiet_ = quiet != 0;
   return 0;
 }
 

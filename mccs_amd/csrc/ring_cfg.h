@@ -98,9 +98,9 @@ struct mccsLaunchGuard {
 // k's works are inline_work[k * channels used ...], each only its header and
 // its one element (mccsInlineWork, 56 B instead of mccsDevWork's 512): HIP
 // copies every argument byte at every launch, and 4 KiB of them cost 1-3 us
-// of host time per launch (profiles/r05_host_overhead.json).  7 works = the
-// n = 8 rings.
-#define MCCS_INLINE_WORKS 7
+// of host time per launch (profiles/r05_host_overhead.json).  8 works: the
+// n = 8 rings (7 channels), or two fused rank slots of 4 channels.
+#define MCCS_INLINE_WORKS 8
 struct mccsInlineWork {
   struct mccsDevWorkHeader header;
   struct mccsDevWorkElem elem;
@@ -208,14 +208,17 @@ static_assert(sizeof(mccsMultiLaunchArgs) <= 1024, "ring launch arguments must s
 struct mccsDirectRank {  // one rank slot of a direct launch (blockIdx.y)
   const void* send;
   void* recv;
-  char* region[MCCS_DIRECT_MAX_RANKS];  // every rank's direct region as this rank maps it
-  struct mccsDevComm* comm;             // the rank's device communicator
-  uint32_t* abort_flag;                 // comm->abortFlag (one load less in the prologue)
+  struct mccsDevComm* comm;  // the rank's device communicator
+  uint32_t* abort_flag;      // comm->abortFlag (one load less in the prologue)
   uint32_t rank;
   uint32_t err_line;
 };
 struct mccsDirectArgs {
   struct mccsDirectRank r[MCCS_MULTI_MAX_RANKS];
+  // every rank's direct region as the launching process maps it: one table
+  // for all rank slots (fused slots are ranks of one communicator in one
+  // process, plan.cpp direct_group), so HIP copies 64 B per launch, not 1 KiB
+  char* region[MCCS_DIRECT_MAX_RANKS];
   uint64_t count;          // elements
   uint64_t slot_bytes;     // bytes of one two-shot slot (>= count * element size for two-shot)
   uint64_t oslot_bytes;    // bytes of one one-shot slot (>= count * element size for one-shot)

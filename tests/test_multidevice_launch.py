@@ -189,10 +189,15 @@ def test_work_list_falls_back_to_the_fifo(fake, monkeypatch):
                                  stream=0)
         launches = [kv for k, kv in _log() if k == "launch"]
         assert len(launches) == 8 and all(kv["inline_works"] == "0" for kv in launches), launches
+        # MCCS_INLINE_WORKS=0 is read when a communicator is created
         monkeypatch.setenv("MCCS_INLINE_WORKS", "0")
-        _allreduce_group(comms)
+        off = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
+        _log()
+        _allreduce_group(off)
         launches = [kv for k, kv in _log() if k == "launch"]
         assert len(launches) == 8 and all(kv["inline_works"] == "0" for kv in launches), launches
+        for c in off:
+            c.destroy()
     finally:
         for c in comms:
             c.destroy()
@@ -209,7 +214,7 @@ def test_colocated_ranks_are_fused_per_device(fake):
         ev = _log()
         launches = _check_launch_phase(ev, 4, 2, comms[0].nchannels * 2)
         assert len(launches) == 4
-        # 2 ranks x 7 channels = 14 works > MCCS_INLINE_WORKS (7): the work FIFO
+        # 2 ranks x 7 channels = 14 works > MCCS_INLINE_WORKS (8): the work FIFO
         assert all(kv["inline_works"] == "0" for _, kv in launches), launches
     finally:
         for c in comms:
@@ -253,11 +258,11 @@ def test_comm_events_ride_on_the_launch(fake, monkeypatch):
     records remain only where something consumes them: the two-stream
     bridge's user events."""
     fake(8)
-    comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
-    try:
-        _log()
-        for inline in ("1", "0"):  # launch-argument works, then the work FIFO
-            monkeypatch.setenv("MCCS_INLINE_WORKS", inline)
+    for inline in ("1", "0"):  # launch-argument works, then the work FIFO (read at creation)
+        monkeypatch.setenv("MCCS_INLINE_WORKS", inline)
+        comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20))
+        try:
+            _log()
             _allreduce_group(comms)
             ev = _log()
             launches = [kv for k, kv in ev if k == "launch"]
@@ -267,9 +272,10 @@ def test_comm_events_ride_on_the_launch(fake, monkeypatch):
                 c.sync()
             waits = [kv["what"] for k, kv in _log() if k == "host_wait"]
             assert waits.count("event") == 8 and "device" not in waits, waits
-    finally:
-        for c in comms:
-            c.destroy()
+        finally:
+            for c in comms:
+                c.destroy()
+    monkeypatch.delenv("MCCS_INLINE_WORKS")
     comms = C.init_all(list(range(8)), C.CommConfig(buffer_size=1 << 20, bridge_streams=1))
     try:
         _log()
@@ -282,11 +288,15 @@ def test_comm_events_ride_on_the_launch(fake, monkeypatch):
             c.destroy()
 
 
-def test_fused_ranks_record_their_events_only_when_consumed(fake):
+@pytest.mark.parametrize("inline", ["1", "0"])
+def test_fused_ranks_record_their_events_only_when_consumed(fake, monkeypatch, inline):
     """Ranks sharing a device run as one launch: the first comm's event rides
     on it; the others' events are recorded only when consumed (here: not), and
     their mccsCommSync waits on the launching comm's event (not the device:
-    ADVICE r03)."""
+    ADVICE r03).  Works in the launch arguments or in the work FIFO alike (a
+    FIFO launch used to record every fused slot's event: a marker packet and
+    ~1.5 us of host time each)."""
+    monkeypatch.setenv("MCCS_INLINE_WORKS", inline)
     fake(4)
     comms = C.init_all([0, 0, 1, 1, 2, 2, 3, 3], C.CommConfig(buffer_size=1 << 20, lanes=2, channel_count=1,
                                                               rings=[[0, 1, 2, 3, 4, 5, 6, 7]]))

@@ -43,11 +43,13 @@ def main():
     st = side_stream(torch, 0, slot=1)
     for n in args.n:
         top = max(args.sizes_kib) << 10
-        sets = {"ring": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1)),
-                "direct": C.init_all([0] * n, C.CommConfig(direct_bytes=top, oneshot_bytes=-1, ll_bytes=-1)),
-                "oneshot": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, ll_bytes=-1,
-                                                            oneshot_bytes=min(top, args.oneshot_max_kib << 10))),
-                "ll": C.init_all([0] * n, C.CommConfig(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=1 << 20))}
+        cfgs = {"ring": C.CommConfig(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=-1),
+                "direct": C.CommConfig(direct_bytes=top, oneshot_bytes=-1, ll_bytes=-1),
+                "oneshot": C.CommConfig(direct_bytes=-1, ll_bytes=-1, oneshot_bytes=min(top, args.oneshot_max_kib << 10)),
+                "ll": C.CommConfig(direct_bytes=-1, oneshot_bytes=-1, ll_bytes=1 << 20)}
+        if len(args.blocks) == 1:
+            os.environ["MCCS_DIRECT_BLOCKS"] = str(args.blocks[0])
+        sets = {a: C.init_all([0] * n, cfg) for a, cfg in cfgs.items()}
         for a in [a for a in sets if a not in args.algos]:
             for c in sets.pop(a):
                 c.destroy()
@@ -62,8 +64,12 @@ def main():
                 if args.allgather and algo == "direct":
                     continue
                 for blocks in (args.blocks if algo != "ring" else [0]):
-                    if blocks:
+                    if blocks and len(args.blocks) > 1:
+                        # MCCS_DIRECT_BLOCKS is read when a communicator is created
                         os.environ["MCCS_DIRECT_BLOCKS"] = str(blocks)
+                        for c in comms:
+                            c.destroy()
+                        comms = sets[algo] = C.init_all([0] * n, cfgs[algo])
 
                     def once():
                         with C.group():

@@ -9,13 +9,32 @@
  *
  *   gcc -std=c11 -O2 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ tools/host_overhead.c \
  *       -Lmccs_amd -lmccs_hip -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,$PWD/mccs_amd -o tools/host_overhead
+ *   tools/host_overhead [calls per size] [--fake]
+ *
+ * --fake (MCCS_TEST_HOOKS=1 in the environment; no GPU): the library's own
+ * host path on the quiet recording fake runtime, every HIP call a no-op --
+ * what the planner, the group state and the launch bookkeeping cost.
  */
-#define _POSIX_C_SOURCE 199309L
+#define _GNU_SOURCE
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include <time.h>
 
 #include "mccs_hip.h"
+
+/* test hooks of libmccs_hip.so (csrc/host/rt.cpp), not part of the header:
+   looked up at run time, so the tool also runs against a library without them */
+typedef int (*hook_fn)(int);
+
+enum { MAXS = 4096 };
+static double one[MAXS];
+static int cmp_double(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : x > y;
+}
 
 static double now_us(void) {
   struct timespec t;
@@ -23,18 +42,28 @@ static double now_us(void) {
   return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
 }
 
-int main(void) {
-  enum { NR = 2, CALLS = 2000 };
+int main(int argc, char** argv) {
+  enum { NR = 2 };
+  /* calls per size (default 2000); fewer than the HIP queue holds keeps the
+     host from waiting for the device, so host_us_per_call is the issue cost */
+  const int CALLS = argc > 1 ? atoi(argv[1]) : 2000;
+  const int fake = argc > 2 && strcmp(argv[2], "--fake") == 0;
+  if (fake) {
+    hook_fn rt = (hook_fn)dlsym(RTLD_DEFAULT, "mccs_test_fake_runtime");
+    hook_fn quiet = (hook_fn)dlsym(RTLD_DEFAULT, "mccs_test_fake_quiet");
+    if (!rt || !quiet || rt(1) != mccsSuccess || quiet(1) != 0) return 6;
+  }
   mccsComm_t comms[NR];
   int devices[NR] = {0, 0};
   if (mccsCommInitAll(comms, NR, devices, NULL) != mccsSuccess) return 1;
-  hipStream_t st;
-  if (hipStreamCreate(&st) != hipSuccess) return 1;
+  hipStream_t st = (hipStream_t)0x7000;  /* a fake stream handle under --fake */
+  if (!fake && hipStreamCreate(&st) != hipSuccess) return 1;
   const size_t sizes[3] = {16 << 10, 512 << 10, 8 << 20};
   void *buf[NR][2];
   for (int r = 0; r < NR; ++r)
     for (int k = 0; k < 2; ++k)
-      if (hipMalloc(&buf[r][k], 8 << 20) != hipSuccess) return 1;
+      if (fake) buf[r][k] = (void*)(uintptr_t)(0x10000000ull * (2 * r + k + 1));
+      else if (hipMalloc(&buf[r][k], 8 << 20) != hipSuccess) return 1;
   printf("{\"what\": \"host time per call: GroupStart + 2 x mccsAllReduce + GroupEnd, 2-rank virtual node, fp32, library defaults\", \"rows\": [");
   for (int s = 0; s < 3; ++s) {
     const size_t count = sizes[s] / 4;
@@ -50,15 +79,37 @@ int main(void) {
         double e = now_us();
         issue += e - a;
         launch += e - b;
+        if (i < MAXS) one[i] = e - a;
       }
-      if (hipStreamSynchronize(st) != hipSuccess) return 4;
+      if (!fake && hipStreamSynchronize(st) != hipSuccess) return 4;
       for (int r = 0; r < NR; ++r)
         if (mccsCommSync(comms[r]) != mccsSuccess) return 5;
       const double wall = now_us() - t0;
+      /* median of single calls, the device drained every 16 calls outside
+         them: the issue cost with no wait for queue space */
+      double med = 0;
+      {
+        const int m = 400;
+        for (int i = 0; i < m; ++i) {
+          if (i % 16 == 0) {
+            if (!fake && hipStreamSynchronize(st) != hipSuccess) return 4;
+          }
+          double a = now_us();
+          mccsGroupStart();
+          for (int r = 0; r < NR; ++r)
+            if (mccsAllReduce(buf[r][0], buf[r][1], count, mccsFloat32, mccsDevSum, comms[r], st) != mccsSuccess)
+              return 2;
+          if (mccsGroupEnd() != mccsSuccess) return 3;
+          one[i] = now_us() - a;
+        }
+        if (!fake && hipStreamSynchronize(st) != hipSuccess) return 4;
+        qsort(one, m, sizeof(double), cmp_double);
+        med = one[m / 2];
+      }
       if (warm)
         printf("%s{\"bytes\": %zu, \"algo\": %d, \"host_us_per_call\": %.2f, \"group_end_us\": %.2f, "
-               "\"wall_us_per_call\": %.2f}", s ? ", " : "", sizes[s], mccsCommLastAlgo(comms[0]), issue / CALLS,
-               launch / CALLS, wall / CALLS);
+               "\"wall_us_per_call\": %.2f, \"host_us_median_drained\": %.2f}", s ? ", " : "", sizes[s],
+               mccsCommLastAlgo(comms[0]), issue / CALLS, launch / CALLS, wall / CALLS, med);
     }
   }
   printf("]}\n");
