@@ -39,12 +39,16 @@ def _streams():
 def _cfg(kind):
     # few workgroups per rank: long-running launches, and two of them (one
     # waiting on the guard) stay far inside the GPU's co-resident slots
-    ll = 1 << 20 if kind == "ll" else -1
-    return C.CommConfig(timeout_ms=20000, lanes=2, channel_count=2, ll_bytes=ll, oneshot_bytes=-1, direct_bytes=-1)
+    return C.CommConfig(timeout_ms=20000, lanes=2, channel_count=2, ll_bytes=1 << 20 if kind == "ll" else -1,
+                        oneshot_bytes=8 << 20 if kind == "oneshot" else -1,
+                        direct_bytes=8 << 20 if kind == "twoshot" else -1)
 
 
 def _small_count(kind):
-    return 30001 if kind == "ll" else 1000003
+    return {"ll": 30001, "oneshot": 300001, "twoshot": 300001}.get(kind, 1000003)
+
+
+ALGO = {"ring": "ring", "ll": "ll", "oneshot": "oneshot", "twoshot": "direct"}
 
 
 def _check(orc, comms, inputs, outs, code, what):
@@ -70,7 +74,7 @@ def _allreduce(comms, send, recv, count, code, stream):
             C.all_reduce(c, send[r], recv[r], count, code, 0, stream=stream)
 
 
-@pytest.mark.parametrize("kind", ["ring", "ll"])
+@pytest.mark.parametrize("kind", ["ring", "ll", "oneshot", "twoshot"])
 @pytest.mark.parametrize("n", [1, 2, 4])
 def test_replay_beside_an_eager_launch(orc, n, kind):
     """A comm's AllReduce captured in a graph on stream B, replayed right after
@@ -78,7 +82,7 @@ def test_replay_beside_an_eager_launch(orc, n, kind):
     the streams): both exact, the guard contended."""
     import torch
 
-    if kind == "ll" and n == 1:
+    if kind != "ring" and n == 1:
         pytest.skip("a one-rank comm has no direct kernel")
     comms = C.init_all([0] * n, _cfg(kind))
     try:
@@ -98,7 +102,7 @@ def test_replay_beside_an_eager_launch(orc, n, kind):
         torch.cuda.synchronize()
         for c in comms:
             c.sync()
-        assert comms[0].last_algo() == ("ll" if kind == "ll" else "ring")
+        assert comms[0].last_algo() == ALGO[kind]
         w0 = _waits(comms)
         for rep in range(4):
             xs = [vnode.gen(code_x, cnt_x, rng) for _ in range(n)]
@@ -164,6 +168,56 @@ def test_two_graphs_replayed_on_two_streams(orc, n):
             _check(orc, comms, xs, rx, F16, f"graph 2 rep {rep}")
             _check(orc, comms, ys, ry, F32, f"graph 1 rep {rep}")
         assert _waits(comms) > w0, "the two replays never met on the guard: no overlap was tested"
+        _idle(comms)
+    finally:
+        torch.cuda.synchronize()
+        vnode.destroy(comms)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_allgather_replay_beside_an_eager_allreduce(orc, n):
+    """The ring AllGather kernel takes the same guard: a captured AllGather
+    replayed beside an eager AllReduce of the same comms, both exact."""
+    import torch
+
+    comms = C.init_all([0] * n, _cfg("ring"))
+    try:
+        rng = np.random.default_rng(90 + n)
+        sa, sb = _streams()
+        size = 1 << 20
+        src = [torch.zeros(size, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        out = [torch.zeros(n * size, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        sy = [vnode.to_dev(np.zeros(BIG, np.float32)) for _ in range(n)]
+        ry = [torch.zeros_like(t) for t in sy]
+        with C.group():
+            for r in range(n):
+                C.all_gather(comms[r], src[r], out[r], size, stream=sb)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=sb):
+            with C.group():
+                for r in range(n):
+                    C.all_gather(comms[r], src[r], out[r], size, stream=sb)
+        torch.cuda.synchronize()
+        w0 = _waits(comms)
+        for rep in range(3):
+            data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(n)]
+            ys = [vnode.gen(F32, BIG, rng) for _ in range(n)]
+            for r in range(n):
+                src[r].copy_(torch.from_numpy(data[r]))
+                sy[r].copy_(torch.from_numpy(ys[r].view(np.uint8).copy()))
+            torch.cuda.synchronize()
+            _allreduce(comms, sy, ry, BIG, F32, sa)
+            with torch.cuda.stream(sb):
+                g.replay()
+            torch.cuda.synchronize()
+            for c in comms:
+                c.sync()
+            exp = np.concatenate(data)
+            for r in range(n):
+                assert np.array_equal(out[r].cpu().numpy(), exp), f"AllGather rep {rep} rank {r}"
+            _check(orc, comms, ys, ry, F32, f"eager rep {rep}")
+        assert _waits(comms) > w0, "the replay never met the eager launch on the guard: no overlap was tested"
         _idle(comms)
     finally:
         torch.cuda.synchronize()
