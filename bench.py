@@ -254,7 +254,14 @@ def bench_reduce(args) -> dict:
     a, b, c = sets[0]
     if args.variant or args.unroll or args.policy >= 0 or args.blocks_per_cu or args.stages or args.waves:
         mccs_amd.tune(args.variant, args.unroll, args.policy, args.blocks_per_cu, args.stages, args.waves)
-    stream = torch.cuda.current_stream()
+    # The timed launches go to a non-blocking side stream of their own (a
+    # collective library's kernels run on the caller's or its own stream, not
+    # the legacy null stream); the events are recorded on that stream.
+    from mccs_amd._streams import side_stream
+
+    stream = side_stream(torch, 0, slot=0)
+    stream.wait_stream(torch.cuda.current_stream())  # the inputs were generated on the default stream
+    torch.cuda.set_stream(stream)
     cur = [0]
 
     def step():
@@ -285,6 +292,11 @@ def bench_reduce(args) -> dict:
     K = args.steps
     t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    # A spin kernel ahead of the start event (outside the timed region) keeps
+    # the GPU busy while the host enqueues the K launches, so the timed
+    # region is K back-to-back steps and not the host's latency to submit the
+    # first one after the synchronize (~5 us, 0.25 us per step at K = 20).
+    torch.cuda._sleep(1_000_000)
     t_start.record(stream)
     for _ in range(K):
         step()
