@@ -149,7 +149,8 @@ static mccsResult_t make_comm(int rank, int nranks, int device, const mccsCommCo
   c->nch = (int)c->rings.size();
   if (const char* v = std::getenv("MCCS_SLICE_STEPS")) c->slice_steps = std::atoi(v) == 2 ? 2 : ALLREDUCE_CHUNKSTEPS;
   if (const char* v = std::getenv("MCCS_INLINE_WORKS")) c->inline_works = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MCCS_DIRECT_BLOCKS")) c->direct_blocks = std::atoi(v) > 0 ? std::atoi(v) : 128;
+  // (at most 4096: a launch guard counts a slot's workgroups in 16 bits)
+  if (const char* v = std::getenv("MCCS_DIRECT_BLOCKS")) c->direct_blocks = std::atoi(v) > 0 ? std::min(std::atoi(v), 4096) : 128;
   c->block_threads = cfg.block_threads;
   // auto lanes: ~64 streaming workgroups per rank (128 at n = 2).  A lane's
   // throughput is bound by its per-slice latency chain (flag poll, loads,
