@@ -272,7 +272,11 @@ def test_replay_beside_an_eager_launch_across_processes():
            "127.0.0.1", "--master-port", str(port), os.path.join(here, "ipc_worker.py")]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", IPC_MODES="guard")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=os.path.dirname(here))
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    # both ranks print to one pipe: their lines can run together, so take
+    # every JSON object from the stream (the merged verdict is rank 0's last)
+    import re
+
+    lines = [json.loads(m) for m in re.findall(r"\{(?:[^{}]|\{[^{}]*\})*\}", r.stdout)]
     assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-3000:]
     res = lines[-1]
     assert res["all_ok"], res
