@@ -5,6 +5,7 @@
 // directly (no daemon process on the hot path: the reference's WR/WC shared
 // memory queues only relay the same arguments, collectives.rs:88-131).
 #include <hip/hip_runtime.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -338,6 +339,12 @@ extern "C" mccsResult_t mccsCommInitAll(mccsComm_t* comms, int nranks, const int
   return mccsSuccess;
 }
 
+// This process's pid namespace (the inode of /proc/self/ns/pid), 0 if unknown.
+static uint64_t pid_namespace() {
+  struct stat st;
+  return stat("/proc/self/ns/pid", &st) == 0 ? (uint64_t)st.st_ino : 0;
+}
+
 // Two connect handles name the same GPU: same host and PCI bus id (ordinals
 // are local to a process, so they would match across different GPUs).
 static bool same_gpu(const ConnectHandle& a, const ConnectHandle& b) {
@@ -386,6 +393,7 @@ extern "C" mccsResult_t mccsCommSetupRank(mccsComm_t* out, int rank, int nranks,
   h.nranks = nranks;
   h.device = device;
   h.pid = (int32_t)getpid();
+  h.pidns = pid_namespace();
   h.fifo_memory = !c->own_arena_uncached                              ? MCCS_FIFO_DEVICE
                   : c->cfg.fifo_memory == MCCS_FIFO_UNCACHED_RELEASE ? MCCS_FIFO_UNCACHED_RELEASE
                                                                      : MCCS_FIFO_UNCACHED;
@@ -476,6 +484,17 @@ extern "C" mccsResult_t mccsCommConnect(mccsComm_t comm, const void* all_handles
         return refuse(b);
       }
     }
+    // From here a peer may map this rank's arena, so its destroy awaits every
+    // peer's release word -- or, for a peer whose exit this process can see
+    // (same host and pid namespace), that peer's exit: a peer that crashed, or
+    // whose Connect failed before it mapped the arena, never writes the word
+    // (ADVICE r05), and once it has exited none of its kernels can write here.
+    const ConnectHandle& me = hs[c->rank];
+    c->peer_pid.assign(c->nranks, 0);
+    for (int r = 0; r < c->nranks; ++r)
+      if (r != c->rank && hs[r].pidns && hs[r].pidns == me.pidns && hs[r].pid > 0 &&
+          std::strncmp(hs[r].host, me.host, sizeof(me.host)) == 0)
+        c->peer_pid[r] = hs[r].pid;
   }
   // Ranks of this communicator that share a GPU as separate processes run
   // separate launches that spin on each other's flags, so all of them must be

@@ -168,6 +168,7 @@ struct PooledArena {
   uint64_t epoch;        // the last tenancy
   size_t release_off;    // its release words (ArenaLayout::release_off of that tenancy)
   uint64_t waiting;      // bit r: rank r's release not seen yet
+  std::vector<int32_t> pid;  // rank r's process where its exit can be seen (0: wait for the word)
 };
 static std::mutex g_pool_mu;
 static std::vector<PooledArena> g_pool;
@@ -193,20 +194,28 @@ static void pool_refresh(Pick pick) {
     char* ptr;
     size_t off;
     uint64_t epoch, waiting;
+    std::vector<int32_t> pid;
   };
   std::vector<Check> todo;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     for (const auto& a : g_pool)
-      if (a.waiting && a.generation == rt_generation() && pick(a)) todo.push_back({a.ptr, a.release_off, a.epoch, a.waiting});
+      if (a.waiting && a.generation == rt_generation() && pick(a))
+        todo.push_back({a.ptr, a.release_off, a.epoch, a.waiting, a.pid});
   }
   if (todo.empty()) return;
   for (auto& t : todo) {
     uint64_t w[ArenaLayout::kReleaseBytes / sizeof(uint64_t)];
     uint64_t released = 0;
-    if (rt().Memcpy(w, t.ptr + t.off, sizeof(w), hipMemcpyDeviceToHost) == hipSuccess)
-      for (int r = 0; r < 64; ++r)
-        if ((t.waiting >> r & 1) && w[r] == t.epoch) released |= 1ull << r;
+    const bool read = rt().Memcpy(w, t.ptr + t.off, sizeof(w), hipMemcpyDeviceToHost) == hipSuccess;
+    for (int r = 0; r < 64; ++r) {
+      if (!(t.waiting >> r & 1)) continue;
+      // its word holds the tenancy, or the peer process exited without
+      // writing it (crashed, or its Connect failed before mapping this
+      // arena): either way none of its kernels can still write here
+      if ((read && w[r] == t.epoch) || (r < (int)t.pid.size() && t.pid[r] > 0 && rt().ProcessGone(t.pid[r])))
+        released |= 1ull << r;
+    }
     t.waiting = released;
   }
   std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -234,9 +243,9 @@ static char* pool_take(int device, bool uncached, size_t need, size_t* got) {
 }
 
 static void pool_give(int device, bool uncached, size_t bytes, char* p, uint64_t epoch = 0, size_t release_off = 0,
-                      uint64_t waiting = 0) {
+                      uint64_t waiting = 0, std::vector<int32_t> pid = {}) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.push_back(PooledArena{rt_generation(), device, uncached, bytes, p, epoch, release_off, waiting});
+  g_pool.push_back(PooledArena{rt_generation(), device, uncached, bytes, p, epoch, release_off, waiting, std::move(pid)});
 }
 
 // Out of device memory: return this device's released pooled uncached arenas
@@ -694,7 +703,7 @@ mccsResult_t comm_free(Comm* c) {
       for (int r = 0; r < c->nranks; ++r)
         if (r != c->rank) waiting |= 1ull << r;
     pool_give(c->device, c->own_arena_uncached, c->own_arena_bytes, c->own_arena, c->arena_epoch,
-              c->layout.release_off(), waiting);
+              c->layout.release_off(), waiting, c->peer_pid);
   }
   for (auto p : c->d_peers)
     if (p) (void)rt().Free(p);

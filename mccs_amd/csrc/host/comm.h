@@ -142,6 +142,9 @@ struct ConnectHandle {
   // this communicator's tenancy of the rank's FIFO arena: peers write it into
   // the arena's release word when they destroy their communicator
   uint64_t arena_epoch;
+  // the rank's pid namespace (inode of /proc/self/ns/pid; 0 unknown): a peer's
+  // pid names a process of this host only within the same namespace
+  uint64_t pidns;
 };
 constexpr uint32_t kHandleMagic = 0x6d636373;  // "mccs"
 // Default FIFO-wait watchdog (mccsCommConfig.timeout_ms = 0): 10 minutes,
@@ -212,6 +215,9 @@ struct Comm {
   uint64_t arena_epoch = 0;
   bool arena_shared = false;
   std::vector<uint64_t> peer_epoch;
+  // each peer's pid where this process can tell whether it is alive (same
+  // host and pid namespace; else 0): a dead peer's release is not awaited
+  std::vector<int32_t> peer_pid;
   std::vector<char*> peer_arena;
   std::vector<bool> peer_opened_ipc;
   bool all_uncached = true;

@@ -4,12 +4,14 @@
 #include "rt.h"
 
 #include <dlfcn.h>
+#include <signal.h>
 #include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -151,6 +153,7 @@ class HipRuntime final : public DeviceRuntime {
   hipError_t IpcCloseMemHandle(void* p) override { return ret(hipIpcCloseMemHandle(p)); }
   hipError_t DeviceGetPCIBusId(char* id, int len, int device) override { return ret(hipDeviceGetPCIBusId(id, len, device)); }
   hipError_t DeviceGetByPCIBusId(int* device, const char* id) override { return ret(hipDeviceGetByPCIBusId(device, id)); }
+  bool ProcessGone(int pid) override { return pid > 0 && kill(pid, 0) != 0 && errno == ESRCH; }
 };
 
 // Recording fake: "device" memory is host memory tagged with its device,
@@ -501,8 +504,19 @@ class FakeRuntime final : public DeviceRuntime {
     *device = (int)bus - 0x10;
     return hipSuccess;
   }
+  // Every fake "process" is this one: a peer pid counts as exited only once a
+  // test says so (mccs_test_fake_process_exit).
+  bool ProcessGone(int pid) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    return std::find(exited_.begin(), exited_.end(), pid) != exited_.end();
+  }
+  void process_exit(int pid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    exited_.push_back(pid);
+  }
 
  private:
+  std::vector<int> exited_;
   struct Block {
     int device;
     bool uncached;
@@ -739,6 +753,16 @@ extern "C" int mccs_test_fake_destroy_graph(int graph) {
     f = mccs::g_fake.load();
   }
   return f ? f->destroy_graph(graph) : -1;
+}
+
+// Marks fake peer process `pid` as exited and reaped (the arena pool's
+// liveness check, DeviceRuntime::ProcessGone); -1 without a fake.
+extern "C" int mccs_test_fake_process_exit(int pid) {
+  std::lock_guard<std::mutex> lk(mccs::g_fake_mu);
+  mccs::FakeRuntime* f = mccs::g_fake.load();
+  if (!f) return -1;
+  f->process_exit(pid);
+  return 0;
 }
 
 // Pooled FIFO arenas of the current runtime still awaiting a peer's release

@@ -70,6 +70,10 @@ class DeviceRuntime {
   virtual hipError_t IpcCloseMemHandle(void* p) = 0;
   virtual hipError_t DeviceGetPCIBusId(char* id, int len, int device) = 0;
   virtual hipError_t DeviceGetByPCIBusId(int* device, const char* id) = 0;
+  // True only when process `pid` (of this host and pid namespace) has exited
+  // and been reaped: its GPU queues are gone, so none of its kernels can still
+  // write a peer's FIFO arena (the arena pool stops waiting for its release).
+  virtual bool ProcessGone(int pid) = 0;
 };
 
 DeviceRuntime& rt();

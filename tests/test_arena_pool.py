@@ -164,3 +164,65 @@ def test_refused_connect_does_not_strand_the_arena(lib):
     assert _calls(lib).count("MallocUncached") == 0  # both arenas were reusable at once
     for c in again:
         c.destroy()
+
+
+def test_exited_peer_is_not_awaited(lib):
+    """a peer that crashed after connecting, or whose Connect
+    failed before it mapped this rank's arena, never writes its release word,
+    and the arena stayed pooled for the life of the process.  A peer of the
+    same host and pid namespace that has exited (and been reaped) can no
+    longer write the arena, so the pool stops awaiting it.  The fake runtime
+    marks a fake peer pid exited on request."""
+    from test_rank_per_process import _connect_per_process
+
+    comms, _ = _connect_per_process(lib, 2)  # rank 0 sees rank 1 as pid 0x7ffffff0 - 1, and vice versa
+    comms[0].destroy()
+    assert lib.mccs_test_pool_waiting() == 1  # rank 1 is alive: its kernels may still post
+    assert lib.mccs_test_fake_process_exit(0x7ffffff0 - 1) == 0
+    assert lib.mccs_test_pool_waiting() == 0  # rank 1 exited: nothing can write rank 0's arena
+    comms[1].destroy()  # rank 0 wrote its release into rank 1's arena at its own destroy
+    assert lib.mccs_test_pool_waiting() == 0
+    _calls(lib)
+    again = C.init_all([0, 1])
+    assert _calls(lib).count("MallocUncached") == 0  # both arenas reusable
+    for c in again:
+        c.destroy()
+
+
+def test_failed_ipc_open_then_peer_exit(lib):
+    """Rank 1's Connect fails opening rank 0's arena (after the handle check,
+    so both arenas were exported and stay awaited); rank 0 connected.  Rank 1
+    never mapped rank 0's arena and never writes its word: rank 0's arena is
+    reusable once rank 1's process has exited, and not before."""
+    from test_rank_per_process import PID_OFFSET
+
+    n = 2
+    hsize = lib.mccsConnectHandleSize()
+    hs, bufs = [], []
+    for r in range(n):
+        buf = (ctypes.c_char * hsize)()
+        h = ctypes.c_void_p()
+        cfg, keep = C.CommConfig().to_c(n)
+        assert lib.mccsCommSetupRank(ctypes.byref(h), r, n, r, ctypes.byref(cfg), buf) == 0
+        del keep
+        hs.append(h)
+        bufs.append(bytearray(buf))
+
+    def handles(r):
+        out = []
+        for q in range(n):
+            b = bytearray(bufs[q])
+            if q != r:
+                b[PID_OFFSET:PID_OFFSET + 4] = (0x7ffffff0 - q).to_bytes(4, "little")
+            out.append(bytes(b))
+        return ctypes.create_string_buffer(b"".join(out), hsize * n)
+
+    assert lib.mccsCommConnect(hs[0], handles(0)) == 0
+    assert lib.mccs_test_fake_fail(b"IpcOpenMemHandle", 1, 1) == 0
+    assert lib.mccsCommConnect(hs[1], handles(1)) != 0
+    assert b"IPC open of rank 0" in lib.mccsGetLastErrorString()
+    assert lib.mccsCommDestroy(hs[1]) == 0  # its arena: rank 0 mapped it and releases it at its destroy
+    assert lib.mccsCommDestroy(hs[0]) == 0
+    assert lib.mccs_test_pool_waiting() == 1  # rank 0's arena: rank 1 (alive) never wrote its word
+    assert lib.mccs_test_fake_process_exit(0x7ffffff0 - 1) == 0
+    assert lib.mccs_test_pool_waiting() == 0
