@@ -229,8 +229,10 @@ mccsResult_t mccsCommAbort(mccsComm_t comm);
  * this rank's own kernel finished, so the arena goes back to a per-process pool
  * but is handed to a new communicator only once every peer has destroyed its
  * side too (each peer's destroy writes a release word into the arena, after
- * its own kernels ended).  A peer that never destroys (a crashed process)
- * leaves the arena pooled and unused. */
+ * its own kernels ended) or has exited: a peer process that never destroys
+ * (it crashed, or its mccsCommConnect failed) stops being awaited once it has
+ * exited and been reaped, where this process can see that (same host and pid
+ * namespace); otherwise the arena stays pooled and unused. */
 mccsResult_t mccsCommDestroy(mccsComm_t comm);
 /* rank, nranks, device, channels, lanes, block threads, fifo memory kind
  * (MCCS_FIFO_*: the hand-off mode the comm's launches run). */

@@ -44,6 +44,12 @@ __global__ void empty_big(Big b) {
 __global__ void empty_small(unsigned long long x) {
   if (threadIdx.x == 1024 && x == 7) __builtin_trap();
 }
+// spins `ticks` of the 100 MHz constant clock (s_memrealtime): a kernel of a
+// known device time, so the next call is issued while it runs
+__global__ void busy(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(1);
+}
 
 // Median host time of one call: each call timed alone, the stream drained
 // every 16 calls outside the timed calls (so the device never falls behind
@@ -112,6 +118,18 @@ int main(int argc, char** argv) {
     row(nm, per_call_us(n, [&] {
           CK(hipExtModuleLaunchKernel(m, 64, 1, 1, 64, 1, 1, 0, st, a, nullptr, nullptr, ev, 0));
         }, st));
+  }
+  // launch+stop of kernels running 2 / 8 / 20 us, back to back on one event
+  // (the LL one-shot's device time is ~8 us, the 8 MiB ring's ~21 us): does
+  // the host cost depend on whether the previous dispatch is still running?
+  for (unsigned long long us : {2ull, 8ull, 20ull}) {
+    unsigned long long ticks = us * 100;
+    void* ab[1] = {&ticks};
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "launch+stop busy %lluus", us);
+    row(nm, per_call_us(n, [&] { CK(hipExtLaunchKernel((const void*)&busy, dim3(1), dim3(64), ab, 0, st, nullptr, ev, 0)); }, st));
+    std::snprintf(nm, sizeof nm, "launch busy %lluus", us);
+    row(nm, per_call_us(n, [&] { CK(hipLaunchKernel((const void*)&busy, dim3(1), dim3(64), ab, 0, st)); }, st));
   }
   row("GetDevice", per_call_us(4 * n, [&] { int d; CK(hipGetDevice(&d)); }, st));
   row("SetDevice(current)", per_call_us(4 * n, [&] { CK(hipSetDevice(dev)); }, st));
