@@ -206,6 +206,10 @@ mccsResult_t mccsCommConnect(mccsComm_t comm, const void *all_handles);
  * that order on its own, so ranks whose replays race other launches of the
  * comm must order those streams themselves (a captured and an eager collective
  * of the same shape could otherwise pair up differently on different ranks).
+ * A launch waiting for the guard keeps its workgroup slots: launches of one
+ * comm pending together on different hardware queues whose grids exceed the
+ * device's co-resident slots can stall until the watchdog (an error, never a
+ * wrong sum).
  * Calls on ONE communicator must come from one thread at a time (group state
  * is per thread); different communicators may be driven from different
  * threads at once. */

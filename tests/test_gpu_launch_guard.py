@@ -253,6 +253,83 @@ def test_guard_is_free_between_launches(orc):
         vnode.destroy(comms)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_random_mix_of_replays_and_eager_launches(orc, seed, monkeypatch):
+    """A seeded mix on one set of comms: some AllReduces captured into small
+    graphs (1-3 each), the rest issued eagerly, then everything issued in a
+    random order on three streams of two priorities with no dependency
+    between them and no sync -- each graph replayed once, each eager call
+    once.  Size routing picks the LL one-shot, one-shot, two-shot or ring per
+    call, so replays and eager launches of every kind meet on the guard in
+    whatever order the GPU runs them; every output is the oracle's, bit for
+    bit, and the guards end free.  Grids stay small (2 channels x 2 lanes,
+    16 direct workgroups per rank): a launch waiting on the guard keeps its
+    workgroup slots, and three fused launches of full-GPU grids could keep
+    the holder's last workgroups from being dispatched."""
+    import torch
+
+    rng = np.random.default_rng(9100 + seed)
+    n = int(rng.integers(2, 5))
+    monkeypatch.setenv("MCCS_DIRECT_BLOCKS", "16")  # read at communicator creation
+    comms = C.init_all([0] * n, C.CommConfig(timeout_ms=20000, lanes=2, channel_count=2, ll_bytes=64 << 10,
+                                            oneshot_bytes=1 << 20, direct_bytes=4 << 20))
+    streams = [torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1), torch.cuda.Stream(priority=0)]
+    try:
+        ops = []  # (code, count, host inputs, send, recv)
+        for _ in range(14):
+            code = int(rng.choice([F32, F16]))
+            count = max(1, int(np.exp(rng.uniform(np.log(64), np.log(12 << 20)))) // vnode.ESIZE[code])
+            xs = [vnode.gen(code, count, rng) for _ in range(n)]
+            send = [vnode.to_dev(x) for x in xs]
+            ops.append((code, count, xs, send, [torch.zeros_like(t) for t in send]))
+        order = [int(i) for i in rng.permutation(len(ops))]
+        graphs, eager, k = [], [], 0
+        while k < len(order):  # about half the ops go into graphs of 1-3
+            take = int(rng.integers(1, 4))
+            if rng.random() < 0.5:
+                graphs.append(order[k:k + take])
+            else:
+                eager.extend([i] for i in order[k:k + take])
+            k += take
+        torch.cuda.synchronize()
+        captured = []
+        cap = streams[1]
+        for members in graphs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                for i in members:
+                    code, count, xs, send, recv = ops[i]
+                    _allreduce(comms, send, recv, count, code, cap)
+            captured.append(g)
+        torch.cuda.synchronize()
+        for _, _, _, _, recv in ops:  # the capture ran nothing; start from zeros all the same
+            for t in recv:
+                t.zero_()
+        torch.cuda.synchronize()
+        items = [("graph", j) for j in range(len(captured))] + [("eager", e[0]) for e in eager]
+        w0 = _waits(comms)
+        for pos in rng.permutation(len(items)):
+            kind, j = items[int(pos)]
+            st = streams[int(rng.integers(0, 3))]
+            if kind == "graph":
+                with torch.cuda.stream(st):
+                    captured[j].replay()
+            else:
+                code, count, xs, send, recv = ops[j]
+                _allreduce(comms, send, recv, count, code, st)
+        torch.cuda.synchronize()
+        for c in comms:
+            c.sync()
+        for i, (code, count, xs, send, recv) in enumerate(ops):
+            _check(orc, comms, xs, recv, code, f"seed {seed} n {n} op {i} count {count} code {code}")
+        _idle(comms)
+        print(f"seed {seed} n {n}: {len(captured)} graphs, {len(eager)} eager, guard waits {_waits(comms) - w0}")
+        del captured
+    finally:
+        torch.cuda.synchronize()
+        vnode.destroy(comms)
+
+
 def test_replay_beside_an_eager_launch_across_processes():
     """One rank per process (the deployment shape: one guard per launch, each
     workgroup claims it for itself): two ranks, a ring and an LL bucket, a

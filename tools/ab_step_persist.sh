@@ -1,5 +1,8 @@
-# A/B of ring step persistence: libraries under abvar/<variant>/ (MCCS_LIB_PATH),
-# 2- and 4-process rehearsals on one GPU, interleaved.
+# A/B of ring step persistence (profiles/r06_step_persist_ab.json): one
+# libmccs_hip.so per variant under abvar/<variant>/ (git-ignored; build each
+# variant in-tree with __graft_entry__.build() and copy it there), loaded
+# through MCCS_LIB_PATH; 2- and 4-process rehearsals on one GPU, interleaved.
+#   gpurun -- 'bash tools/ab_step_persist.sh'
 set -e
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 for i in 1 2 3; do
