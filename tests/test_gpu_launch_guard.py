@@ -255,8 +255,9 @@ def test_guard_is_free_between_launches(orc):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_random_mix_of_replays_and_eager_launches(orc, seed, monkeypatch):
-    """A seeded mix on one set of comms: some AllReduces captured into small
-    graphs (1-3 each), the rest issued eagerly, then everything issued in a
+    """A seeded mix on one set of comms: some collectives (AllReduces, and
+    AllGathers about one in five) captured into small graphs (1-3 each), the
+    rest issued eagerly, then everything issued in a
     random order on three streams of two priorities with no dependency
     between them and no sync -- each graph replayed once, each eager call
     once.  Size routing picks the LL one-shot, one-shot, two-shot or ring per
@@ -275,13 +276,29 @@ def test_random_mix_of_replays_and_eager_launches(orc, seed, monkeypatch):
                                             oneshot_bytes=1 << 20, direct_bytes=4 << 20))
     streams = [torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1), torch.cuda.Stream(priority=0)]
     try:
-        ops = []  # (code, count, host inputs, send, recv)
+        ops = []  # (code or None for an AllGather, count / bytes per rank, host inputs, send, recv)
         for _ in range(14):
+            if rng.random() < 0.2:
+                nbytes = int(np.exp(rng.uniform(np.log(64), np.log(4 << 20))))
+                xs = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(n)]
+                ops.append((None, nbytes, xs, [vnode.to_dev(x) for x in xs],
+                            [vnode.to_dev(np.zeros(n * nbytes, np.uint8)) for _ in range(n)]))
+                continue
             code = int(rng.choice([F32, F16]))
             count = max(1, int(np.exp(rng.uniform(np.log(64), np.log(12 << 20)))) // vnode.ESIZE[code])
             xs = [vnode.gen(code, count, rng) for _ in range(n)]
             send = [vnode.to_dev(x) for x in xs]
             ops.append((code, count, xs, send, [torch.zeros_like(t) for t in send]))
+
+        def issue(i, st):
+            code, count, xs, send, recv = ops[i]
+            if code is None:
+                with C.group():
+                    for r, c in enumerate(comms):
+                        C.all_gather(c, send[r], recv[r], count, stream=st)
+            else:
+                _allreduce(comms, send, recv, count, code, st)
+
         order = [int(i) for i in rng.permutation(len(ops))]
         graphs, eager, k = [], [], 0
         while k < len(order):  # about half the ops go into graphs of 1-3
@@ -298,8 +315,7 @@ def test_random_mix_of_replays_and_eager_launches(orc, seed, monkeypatch):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=cap):
                 for i in members:
-                    code, count, xs, send, recv = ops[i]
-                    _allreduce(comms, send, recv, count, code, cap)
+                    issue(i, cap)
             captured.append(g)
         torch.cuda.synchronize()
         for _, _, _, _, recv in ops:  # the capture ran nothing; start from zeros all the same
@@ -315,13 +331,18 @@ def test_random_mix_of_replays_and_eager_launches(orc, seed, monkeypatch):
                 with torch.cuda.stream(st):
                     captured[j].replay()
             else:
-                code, count, xs, send, recv = ops[j]
-                _allreduce(comms, send, recv, count, code, st)
+                issue(j, st)
         torch.cuda.synchronize()
         for c in comms:
             c.sync()
         for i, (code, count, xs, send, recv) in enumerate(ops):
-            _check(orc, comms, xs, recv, code, f"seed {seed} n {n} op {i} count {count} code {code}")
+            what = f"seed {seed} n {n} op {i} count {count} code {code}"
+            if code is None:
+                exp = orc.ring_allgather(xs)
+                for r in range(n):
+                    assert np.array_equal(recv[r].cpu().numpy(), exp), f"{what}: rank {r} differs from the oracle"
+            else:
+                _check(orc, comms, xs, recv, code, what)
         _idle(comms)
         print(f"seed {seed} n {n}: {len(captured)} graphs, {len(eager)} eager, guard waits {_waits(comms) - w0}")
         del captured
