@@ -226,3 +226,38 @@ def test_failed_ipc_open_then_peer_exit(lib):
     assert lib.mccs_test_pool_waiting() == 1  # rank 0's arena: rank 1 (alive) never wrote its word
     assert lib.mccs_test_fake_process_exit(0x7ffffff0 - 1) == 0
     assert lib.mccs_test_pool_waiting() == 0
+
+
+def test_peer_in_another_pid_namespace_is_awaited(lib):
+    """A peer pid names a process of this host only within this process's pid
+    namespace: a peer whose handle carries another namespace is awaited by
+    its release word alone, even if a process of that number exits here."""
+    from test_rank_per_process import PID_OFFSET
+
+    n = 2
+    hsize = lib.mccsConnectHandleSize()
+    hs, bufs = [], []
+    for r in range(n):
+        buf = (ctypes.c_char * hsize)()
+        h = ctypes.c_void_p()
+        cfg, keep = C.CommConfig().to_c(n)
+        assert lib.mccsCommSetupRank(ctypes.byref(h), r, n, r, ctypes.byref(cfg), buf) == 0
+        del keep
+        hs.append(h)
+        bufs.append(bytearray(buf))
+    pidns = int.from_bytes(bufs[1][hsize - 8:hsize], "little")  # ConnectHandle.pidns, the last field
+    assert pidns != 0, "this host exposes /proc/self/ns/pid"
+    bufs[1][hsize - 8:hsize] = (pidns ^ 1).to_bytes(8, "little")  # rank 1 "in another namespace"
+    for r in range(n):
+        mine = []
+        for q in range(n):
+            b = bytearray(bufs[q])
+            if q != r:
+                b[PID_OFFSET:PID_OFFSET + 4] = (0x7ffffff0 - q).to_bytes(4, "little")
+            mine.append(bytes(b))
+        assert lib.mccsCommConnect(hs[r], ctypes.create_string_buffer(b"".join(mine), hsize * n)) == 0
+    assert lib.mccsCommDestroy(hs[0]) == 0
+    assert lib.mccs_test_fake_process_exit(0x7ffffff0 - 1) == 0
+    assert lib.mccs_test_pool_waiting() == 1  # rank 1's pid means nothing here: wait for its word
+    assert lib.mccsCommDestroy(hs[1]) == 0  # its word arrives
+    assert lib.mccs_test_pool_waiting() == 0
