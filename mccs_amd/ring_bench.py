@@ -671,8 +671,8 @@ def cpu_ring_baseline(world: int, nbytes: int, nchannels: int, budget_s: float =
 # The ring's only counter-measured traffic: the n = 2 virtual node (one GPU,
 # rocprofv3 FETCH_SIZE / WRITE_SIZE with the gfx950 corrections), carried in
 # the N > 1 line under its own name so nobody reads it as a node measurement.
-VNODE_N2_TRAFFIC = {"traffic_over_algorithmic": 1.0045, "where": "n = 2 virtual node (both ranks on one MI355X), "
-                    "128 MiB fp32, rocprofv3 PMC", "source": "profiles/r04_ring_vnode_summary.json pmc_n2 (r03: 1.0043)"}
+VNODE_N2_TRAFFIC = {"traffic_over_algorithmic": 1.0042, "where": "n = 2 virtual node (both ranks on one MI355X), "
+                    "128 MiB fp32, rocprofv3 PMC", "source": "profiles/r06_ring_vnode_summary.json pmc_n2 (r04: 1.0045)"}
 TRAFFIC_NOT_MEASURED = ("not measured on the node: the PMC passes run on the 1-GPU box only (no 8-GPU box is "
                         "available to this repo's runs); see traffic_virtual_node_n2 for the one measured ratio")
 

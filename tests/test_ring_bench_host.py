@@ -61,8 +61,8 @@ def test_ring_line_schema(share):
     # ratio (virtual node) under its own name
     assert rf["traffic"] is None and rf["traffic_note"].startswith("not measured on the node")
     tv = rf["traffic_virtual_node_n2"]
-    assert tv["traffic_over_algorithmic"] == 1.0045 and "virtual node" in tv["where"]
-    assert tv["source"].startswith("profiles/r04_ring_vnode_summary.json")
+    assert tv["traffic_over_algorithmic"] == 1.0042 and "virtual node" in tv["where"]
+    assert tv["source"].startswith("profiles/r06_ring_vnode_summary.json")
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and 0 < rf["frac"] <= 1
     if share:
         assert rf["peak"] == 8000.0 and abs(rf["achieved"] - 44 * (128 << 20) / 1.2e-3 / 1e9) < 0.01
